@@ -1,0 +1,414 @@
+"""CPU oracle for the Rydberg-CZ Lindblad path -- TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product: only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it.
+The product path (``noisyquantumsimulator_amd``) never routes through it.
+
+It restates, in plain numpy/scipy, the reference solver path of
+scottjones03/NoisyQuantumSimulator for the two-atom Rydberg CZ gate:
+
+* two-atom Hamiltonian        RG/hamiltonians.py:584-1172 (build_laser/detuning/
+                              interaction/zeeman/stark, build_full_hamiltonian) and
+                              RG/hamiltonians.py:1179-1274 (phase-modulated H)
+* collapse operators          RG/noise_models.py:1199-1620 (build_all_noise_operators)
+* time evolution              RG/simulation.py:647-690 (evolve_state -> qutip.mesolve),
+                              evolvers :693-776 (LP square), :1502-1760 (smooth JP),
+                              :1795-1943 (bang-bang JP), :2099-2231 (shaped LP)
+* CZ fidelity                 RG/simulation.py:186-633 (compute_state_fidelity,
+                              compute_CZ_fidelity)
+
+(RG = src/qpu_simulator/micro_physics/neutral_atoms/rydberg_gates.)
+
+Two integrators are provided for every segment:
+
+``method="expm"``   exact propagator exp(L dt) of the column-stacked Liouvillian
+                    (scipy.linalg.expm) -- ground truth, used for parity.
+``method="zvode"``  scipy ZVODE Adams at the reference's tolerances
+                    (atol 1e-10, rtol 1e-8, reference nsteps), restarted per
+                    segment and stepped through the reference's tlist -- the
+                    "QuTiP-like" CPU baseline.  QuTiP itself is an unpinned
+                    third-party dependency (qutip>=5.0.0, pyproject.toml:38) that
+                    is absent here; QuTiP 5's default mesolve integrator wraps the
+                    same scipy ZVODE Adams method on the same vectorised
+                    Liouvillian.
+
+Parity pins (tests/test_oracle_golden.py): the published noise-free fidelities
+of the reference notebooks and the closed-form decay
+known-answer test of scripts/archive/test_mesolve_direct.py:34-51.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import scipy.linalg as sla
+from scipy.integrate import ode
+
+LABELS = ("00", "01", "10", "11")
+
+# --------------------------------------------------------------------------
+# single-atom operators (RG/hamiltonians.py:424-522)
+# --------------------------------------------------------------------------
+
+
+def _ket(d: int, i: int) -> np.ndarray:
+    v = np.zeros(d, dtype=complex)
+    v[i] = 1.0
+    return v
+
+
+def _proj(d: int, i: int) -> np.ndarray:
+    return np.outer(_ket(d, i), _ket(d, i))
+
+
+def _trans(d: int, to: int, frm: int) -> np.ndarray:
+    """|to><frm|"""
+    return np.outer(_ket(d, to), _ket(d, frm))
+
+
+def _two(op1: np.ndarray, op2: np.ndarray) -> np.ndarray:
+    """op1 (x) op2 -- qutip.tensor ordering (atom 1 is the slow index)."""
+    return np.kron(op1, op2)
+
+
+# --------------------------------------------------------------------------
+# Hamiltonian (RG/hamiltonians.py:584-1274)
+# --------------------------------------------------------------------------
+
+
+def two_atom_hamiltonian(Omega: complex, Delta: float, V: float, dim: int = 3,
+                         delta_zeeman: float = 0.0, delta_stark: float = 0.0,
+                         trap_laser_on: bool = True,
+                         add_detuning: bool = True) -> np.ndarray:
+    """H = sum_atoms [ (Omega/2)|r><1| + h.c. - Delta P_r + (dz + ds) P_1 ] + V P_rr.
+
+    dim 4 follows the sigma+ default of RG/hamiltonians.py:655-663 (|r-> not
+    driven), detuning -Delta on both r+ and r- (:741-753, zeeman_splitting=0) and
+    V on every r(+-)r(+-) pair (:835-853).  ``add_detuning=False`` mirrors the
+    phase-modulated builder's ``if Delta != 0`` guard (:1264-1265) -- numerically
+    identical, kept for fidelity to the reference.
+    """
+    d = dim
+    I = np.eye(d, dtype=complex)
+    if d == 3:
+        s1r = _trans(3, 2, 1)              # |r><1|
+        Ha = 0.5 * (Omega * s1r + np.conj(Omega) * s1r.conj().T)
+        Pr = [_proj(3, 2)]
+    elif d == 4:
+        s1rp = _trans(4, 2, 1)             # |r+><1|
+        Ha = 0.5 * (Omega * s1rp + np.conj(Omega) * s1rp.conj().T)
+        Pr = [_proj(4, 2), _proj(4, 3)]
+    else:
+        raise ValueError(f"Unsupported Hilbert space dimension: {dim}. Use 3 or 4.")
+    H = _two(Ha, I) + _two(I, Ha)
+    if add_detuning:
+        for P in Pr:
+            H = H - Delta * (_two(P, I) + _two(I, P))
+    for Pa in Pr:
+        for Pb in Pr:
+            H = H + V * _two(Pa, Pb)
+    P1 = _proj(d, 1)
+    if delta_zeeman != 0:
+        H = H + delta_zeeman * (_two(P1, I) + _two(I, P1))
+    if delta_stark != 0 and trap_laser_on:
+        H = H + delta_stark * (_two(P1, I) + _two(I, P1))
+    return H
+
+
+# --------------------------------------------------------------------------
+# collapse operators (RG/noise_models.py:1199-1620)
+# --------------------------------------------------------------------------
+
+RATE_KEYS = ("gamma_r", "gamma_bbr", "gamma_phi_laser", "gamma_phi_thermal",
+             "gamma_phi_zeeman", "gamma_loss_antitrap", "gamma_loss_background",
+             "gamma_scatter_intermediate", "gamma_leakage", "mJ_leakage_rate")
+
+
+def collapse_operators(rates: Dict[str, float], dim: int = 3,
+                       branching_1: float = 0.5) -> List[np.ndarray]:
+    """The reference's c_op list, in the reference's order and with its
+    ``rate > 0`` guards (build_all_noise_operators, RG/noise_models.py:1575-1592)."""
+    g = {k: float(rates.get(k, 0.0) or 0.0) for k in RATE_KEYS}
+    d = dim
+    I = np.eye(d, dtype=complex)
+    c: List[np.ndarray] = []
+    rys = [2] if d == 3 else [2, 3]
+
+    def both(op, rate):
+        return [math.sqrt(rate) * _two(op, I), math.sqrt(rate) * _two(I, op)]
+
+    # 1. decay (build_decay_operators :1199-1297); per Rydberg state:
+    #    [r->1 (atom1, atom2), r->0 (atom1, atom2)]
+    if g["gamma_r"] > 0:
+        for r in rys:
+            c += both(_trans(d, 1, r), g["gamma_r"] * branching_1)
+            c += both(_trans(d, 0, r), g["gamma_r"] * (1 - branching_1))
+    if g["gamma_bbr"] > 0:
+        for r in rys:
+            c += both(_trans(d, 0, r), g["gamma_bbr"])
+    if d == 4 and g["mJ_leakage_rate"] > 0:
+        c += both(_trans(d, 3, 2), g["mJ_leakage_rate"])
+        c += both(_trans(d, 2, 3), g["mJ_leakage_rate"])
+    # 2. dephasing (:1300-1356)
+    gphi = g["gamma_phi_laser"] + g["gamma_phi_thermal"] + g["gamma_phi_zeeman"]
+    if gphi > 0:
+        for r in rys:
+            c += both(_proj(d, r), gphi)
+    # 3./4./6. losses |r> -> |0>  (:1359-1412)
+    for key in ("gamma_loss_antitrap", "gamma_loss_background"):
+        if g[key] > 0:
+            for r in rys:
+                c += both(_trans(d, 0, r), g[key])
+    # 5. scattering: dephasing of |1> (:1415-1446)
+    if g["gamma_scatter_intermediate"] > 0:
+        c += both(_proj(d, 1), g["gamma_scatter_intermediate"])
+    if g["gamma_leakage"] > 0:
+        for r in rys:
+            c += both(_trans(d, 0, r), g["gamma_leakage"])
+    return c
+
+
+# --------------------------------------------------------------------------
+# Liouvillian + integrators (qutip.mesolve restatement)
+# --------------------------------------------------------------------------
+
+
+def liouvillian(H: np.ndarray, c_ops: Sequence[np.ndarray]) -> np.ndarray:
+    """Column-stacked (QuTiP) superoperator: vec(rho)[a + D*b] = rho[a, b]."""
+    D = H.shape[0]
+    Id = np.eye(D, dtype=complex)
+    L = -1j * (np.kron(Id, H) - np.kron(H.T, Id))
+    for c in c_ops:
+        cdc = c.conj().T @ c
+        L = L + np.kron(c.conj(), c) - 0.5 * np.kron(Id, cdc) - 0.5 * np.kron(cdc.T, Id)
+    return L
+
+
+def vec(rho: np.ndarray) -> np.ndarray:
+    return rho.reshape(-1, order="F")
+
+
+def unvec(v: np.ndarray, D: int) -> np.ndarray:
+    return v.reshape(D, D, order="F")
+
+
+def _zvode(f, y0: np.ndarray, tlist: np.ndarray, atol: float, rtol: float,
+           nsteps: int) -> np.ndarray:
+    r = ode(f)
+    r.set_integrator("zvode", method="adams", atol=atol, rtol=rtol,
+                     nsteps=nsteps, order=12)
+    r.set_initial_value(y0, tlist[0])
+    y = y0
+    for t in tlist[1:]:
+        y = r.integrate(t)
+        if not r.successful():
+            raise RuntimeError("ZVODE failed (excess work / nsteps cap) at t=%g" % t)
+    return y
+
+
+def evolve_state(H: np.ndarray, psi0: np.ndarray, tlist: np.ndarray,
+                 c_ops: Sequence[np.ndarray] = (), method: str = "expm",
+                 options: Optional[dict] = None) -> np.ndarray:
+    """RG/simulation.py:647-690.  A ket with no c_ops stays a ket (Schrodinger);
+    a ket with c_ops becomes rho0 = |psi><psi| (scripts/archive/test_mesolve.py:17-31)."""
+    opts = {"atol": 1e-10, "rtol": 1e-8, "nsteps": 50000}
+    if options:
+        opts.update(options)
+    tlist = np.asarray(tlist, dtype=float)
+    T = tlist[-1] - tlist[0]
+    D = H.shape[0]
+    is_ket = psi0.ndim == 1
+    if is_ket and len(c_ops) == 0:
+        if method == "expm":
+            return sla.expm(-1j * H * T) @ psi0
+        return _zvode(lambda t, y: -1j * (H @ y), psi0.astype(complex), tlist,
+                      opts["atol"], opts["rtol"], opts["nsteps"])
+    rho = np.outer(psi0, psi0.conj()) if is_ket else psi0
+    L = liouvillian(H, c_ops)
+    if method == "expm":
+        return unvec(sla.expm(L * T) @ vec(rho), D)
+    y = _zvode(lambda t, y: L @ y, vec(rho).astype(complex), tlist,
+               opts["atol"], opts["rtol"], opts["nsteps"])
+    return unvec(y, D)
+
+
+# --------------------------------------------------------------------------
+# protocol schedules (RG/simulation.py evolvers)
+# --------------------------------------------------------------------------
+
+
+@dataclass
+class PointSpec:
+    """Physics-level inputs of one simulate_CZ_gate point (after host derivation)."""
+    protocol: str                   # "lp_square" | "lp_shaped" | "bangbang" | "smooth_jp"
+    Omega: float
+    V: float
+    Delta: float = 0.0              # LP static detuning / smooth-JP two-photon detuning
+    delta_zeeman: float = 0.0
+    delta_stark: float = 0.0
+    trap_laser_on: bool = True
+    dim: int = 3
+    # LP
+    tau: float = 0.0                # single pulse (LP) or total (JP) duration
+    xi: complex = 1.0 + 0j
+    pulse_shape: str = "square"
+    area_correction: float = 1.0
+    # bang-bang
+    omega_tau: float = 0.0
+    switching_times: Sequence[float] = ()
+    phases: Sequence[float] = ()
+    # smooth JP
+    A: float = 0.0
+    omega_mod: float = 0.0
+    phi_offset: float = 0.0
+    n_steps: int = 300
+    # noise
+    c_ops: List[np.ndarray] = field(default_factory=list)
+
+
+def initial_kets(dim: int = 3) -> Dict[str, np.ndarray]:
+    b0, b1 = _ket(dim, 0), _ket(dim, 1)
+    return {"00": np.kron(b0, b0), "01": np.kron(b0, b1),
+            "10": np.kron(b1, b0), "11": np.kron(b1, b1)}
+
+
+def cosine_envelope(t: float, tau: float) -> float:
+    """RG/pulse_shaping.py:191-236 (sin^2).  Gaussian and blackman normalise by
+    their own max, so a scalar t gives exactly 1 (:183-186, :290-293)."""
+    return math.sin(math.pi * t / tau) ** 2
+
+
+def envelope(shape: str, t: float, tau: float) -> float:
+    s = shape.lower()
+    if s == "cosine":
+        return float(np.sin(np.pi * t / tau) ** 2)
+    if s in ("gaussian", "blackman", "square"):
+        return 1.0
+    if s == "drag":
+        raise TypeError("pulse_envelope_drag() missing 1 required positional argument: 'Delta_leak'")
+    raise ValueError(f"Unknown pulse shape: {shape}")
+
+
+def segments(p: PointSpec) -> List[Tuple[np.ndarray, np.ndarray, Optional[dict]]]:
+    """(H, tlist, options) per mesolve call, exactly as the reference evolvers."""
+    dz, ds, tl = p.delta_zeeman, p.delta_stark, p.trap_laser_on
+    segs = []
+    if p.protocol == "lp_square":                       # :693-776
+        H1 = two_atom_hamiltonian(p.Omega, p.Delta, p.V, p.dim, dz, ds, tl)
+        H2 = two_atom_hamiltonian(p.Omega * p.xi, p.Delta, p.V, p.dim, dz, ds, tl)
+        t = np.linspace(0, p.tau, 100)
+        segs = [(H1, t, None), (H2, t, None)]
+    elif p.protocol == "lp_shaped":                     # :2099-2231
+        n = 500
+        t_pulse = np.linspace(0, p.tau, n)
+        dt = p.tau / n
+        Om_peak = p.Omega * p.area_correction
+        opts = {"atol": 1e-10, "rtol": 1e-8, "nsteps": 50000}
+        for fac in (1.0, p.xi):
+            for i in range(n - 1):
+                t_mid = (t_pulse[i] + t_pulse[i + 1]) / 2
+                Om_t = Om_peak * envelope(p.pulse_shape, t_mid, p.tau) * fac
+                H = two_atom_hamiltonian(Om_t, p.Delta, p.V, p.dim, dz, ds, tl)
+                segs.append((H, np.array([0.0, dt]), opts))
+    elif p.protocol == "bangbang":                      # :1795-1943
+        bounds = [b / p.Omega for b in [0.0] + list(p.switching_times) + [p.omega_tau]]
+        opts = {"atol": 1e-10, "rtol": 1e-8, "nsteps": 10000}
+        for k, ph in enumerate(p.phases):
+            dts = bounds[k + 1] - bounds[k]
+            if dts < 1e-18:
+                continue
+            H = two_atom_hamiltonian(p.Omega * np.exp(1j * ph), 0.0, p.V, p.dim, dz, ds, tl,
+                                     add_detuning=False)
+            segs.append((H, np.linspace(0, dts, 51), opts))
+    elif p.protocol == "smooth_jp":                     # :1502-1760
+        tl_full = np.linspace(0, p.tau, p.n_steps + 1)
+        dt = p.tau / p.n_steps
+        opts = {"atol": 1e-10, "rtol": 1e-8, "nsteps": 10000}
+        for i in range(p.n_steps):
+            t_mid = tl_full[i] + dt / 2
+            ph = p.A * np.cos(p.omega_mod * t_mid - p.phi_offset)
+            H = two_atom_hamiltonian(p.Omega * np.exp(1j * ph), p.Delta, p.V, p.dim, dz, ds, tl,
+                                     add_detuning=(p.Delta != 0))
+            segs.append((H, np.array([0.0, dt]), opts))
+    else:
+        raise ValueError(p.protocol)
+    return segs
+
+
+def run_point(p: PointSpec, method: str = "expm") -> Dict[str, np.ndarray]:
+    """Final state per computational-basis input (kets if no c_ops, else rho)."""
+    segs = segments(p)
+    out = {}
+    for lab, psi0 in initial_kets(p.dim).items():
+        s = psi0
+        for H, t, opts in segs:
+            s = evolve_state(H, s, t, p.c_ops, method=method, options=opts)
+        out[lab] = s
+    return out
+
+
+# --------------------------------------------------------------------------
+# CZ fidelity (RG/simulation.py:186-633)
+# --------------------------------------------------------------------------
+
+
+def _angle(z: complex) -> float:
+    return float(np.angle(z))
+
+
+def cz_fidelity(results: Dict[str, np.ndarray], dim: int = 3,
+                eigh=np.linalg.eigh) -> Tuple[Dict[str, float], float, Dict]:
+    """Restatement of compute_CZ_fidelity(extract_global_phase=True).
+
+    Mixed branch: F_x = <x|rho_x|x> (qutip.fidelity(rho, |t><t|)**2, the target
+    sign is irrelevant); phase from the dominant eigenvector (gauge-dependent,
+    SURVEY.md hard part 3).  Pure branch: F_x = |<x|psi_x>|^2, phases from
+    overlaps.  F11 gets the cos^2(err/2) controlled-phase penalty in both.
+    """
+    kets = initial_kets(dim)
+    idx = {k: int(np.argmax(np.abs(v))) for k, v in kets.items()}
+    mixed = results["01"].ndim == 2
+    info: Dict = {}
+    fid: Dict[str, float] = {}
+    if mixed:
+        ph = {}
+        for lab in LABELS:
+            rho = results[lab]
+            w, U = eigh(rho)
+            vmax = U[:, int(np.argmax(w))]
+            ph[lab] = _angle(vmax[idx[lab]])
+            fid[lab] = float(np.real(rho[idx[lab], idx[lab]]))
+        cp = ph["11"] - ph["01"] - ph["10"] + ph["00"]
+        info.update(phi_01_rad=ph["01"], phi_11_rad=ph["11"], is_mixed_state=True)
+    else:
+        ov = {lab: complex(results[lab][idx[lab]]) for lab in LABELS}
+        for lab in LABELS:
+            fid[lab] = float(abs(ov[lab]) ** 2)
+        cp = (_angle(ov["11"]) - _angle(ov["01"]) - _angle(ov["10"]) + _angle(ov["00"]))
+        info.update(phi_01_rad=_angle(ov["01"]), phi_11_rad=_angle(-ov["11"]),
+                    amp_01=abs(ov["01"]), amp_11=abs(ov["11"]), is_mixed_state=False)
+    cp = (cp + np.pi) % (2 * np.pi) - np.pi
+    err = min(abs(cp - np.pi), abs(cp + np.pi))
+    pen = float(np.cos(err / 2) ** 2)
+    info.update(controlled_phase_rad=cp, controlled_phase_deg=float(np.degrees(cp)),
+                phase_error_from_pi_rad=err, phase_error_from_pi_deg=float(np.degrees(err)),
+                cz_phase_fidelity=pen, F11_population=fid["11"])
+    fid["11"] = fid["11"] * pen
+    info["F11_with_phase"] = fid["11"]
+    avg = float(np.mean([fid[k] for k in LABELS]))
+    return fid, avg, info
+
+
+def decay_kat(gamma: float, t: np.ndarray, method: str = "expm") -> np.ndarray:
+    """scripts/archive/test_mesolve_direct.py:34-51: H = 0, one decay op
+    sqrt(gamma)|0><1| on a qubit starting in |1>: rho_11(t) = exp(-gamma t)."""
+    H = np.zeros((2, 2), dtype=complex)
+    c = [math.sqrt(gamma) * np.outer(_ket(2, 0), _ket(2, 1))]
+    psi = _ket(2, 1)
+    out = []
+    for tt in t:
+        rho = evolve_state(H, psi, np.array([0.0, tt]), c, method=method)
+        out.append(np.real(rho[1, 1]))
+    return np.array(out)
