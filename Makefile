@@ -1,0 +1,25 @@
+# Build the HIP engine in-tree (the .so travels to the GPU box with the snapshot).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := noisyquantumsimulator_amd
+SO := $(PKG)/libryd_engine.so
+SRC := $(PKG)/csrc/ryd_engine.hip
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-function \
+            -ffp-contract=fast -munsafe-fp-atomics
+
+all: $(SO)
+
+$(SO): $(SRC) include/ryd_engine.h
+	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)
+
+resource-usage: $(SRC)
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -o /tmp/ryd_ru.so $(SRC) 2>&1 | \
+	  grep -E "Function Name|VGPRs:|AGPRs|ScratchSize|Occupancy|SGPRs:" 
+
+asm: $(SRC)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC --cuda-device-only -S -o /tmp/ryd_engine.s $(SRC)
+
+clean:
+	rm -f $(SO)
+
+.PHONY: all clean resource-usage asm

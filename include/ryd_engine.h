@@ -1,0 +1,189 @@
+/*
+ * ryd_engine.h -- C-ABI of the MI355X batched Lindblad engine for the
+ * two-atom Rydberg CZ gate (libryd_engine.so, loaded through ctypes).
+ *
+ * Drop-in boundary.  The reference has no FFI; its replaceable seams are plain
+ * Python functions:
+ *   evolve_state(H, psi0, tlist, c_ops, options) -> Qobj
+ *       src/qpu_simulator/micro_physics/neutral_atoms/rydberg_gates/simulation.py:647-690
+ *       (one state, one segment per call -> qutip.mesolve :689)
+ *   evolve_two_pulse[_lp]  :693-776, evolve_smooth_sinusoidal_jp :1502-1760,
+ *   evolve_bangbang_jp :1795-1943, evolve_shaped_pulse :2099-2231
+ *       (the per-protocol loops over the 4 basis inputs and all segments)
+ * ryd_run_batch() replaces ALL of these for a whole sweep: every parameter
+ * point x 4 computational-basis inputs x every segment of the protocol, in one
+ * launch.  The Python host layer (noisyquantumsimulator_amd.simulation) keeps
+ * simulate_CZ_gate()'s signature (:2534-2567) on top of it.
+ *
+ * Data layout (all float64, structure-of-arrays so lanes read coalesced):
+ *   params  [RYD_NPARAM][ld_params]     column f of point i at params[f*ld + i]
+ *   state   [width][ld_state]           one row per (point, input) lane,
+ *                                       lane = 4*i + input, input = 2*a1 + a2
+ *                                       (labels "00","01","10","11")
+ *   summary [RYD_NSUMMARY][ld_summary]  per point
+ *   status  [n]                         RYD_STATUS_* bits per point
+ * Lindblad state rows: the 25 real coordinates R[i][j] (i: atom 1, j: atom 2)
+ * of rho = sum_ij R[i][j] e_i (x) e_j over the single-atom Hermitian basis
+ * e = {|0><0|, |1><1|, |r><r|, |1><r|+|r><1|, i(|1><r|-|r><1|)}.  This is the
+ * exact invariant sector of the 4 basis inputs (each atom's {1,r}-excitation
+ * number is conserved by H and every c_op of RG/noise_models.py:1449-1620);
+ * every other element of rho is structurally zero, as in QuTiP.  The host
+ * expands it to the QuTiP column-stacked 9x9 rho (noisyquantumsimulator_amd.engine).
+ * Ket state rows: 9 complex amplitudes, interleaved (re, im), basis 3*a1 + a2.
+ *
+ * Ownership/threading: the caller owns every buffer; the library never keeps a
+ * pointer after return (device-buffer calls: until the stream work completes).
+ * One handle per host thread.  Errors: negative return + ryd_last_error()
+ * (thread-local).  Per-point failures never abort a batch: they set status bits
+ * (the analogue of the reference's exception -> 1e6/NaN sentinels,
+ * RG/optimize_cz_gate.py:1174-1177, examples/research_parameter_sweeps.py:133-135).
+ */
+#ifndef RYD_ENGINE_H
+#define RYD_ENGINE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RYD_ABI_VERSION 1
+
+/* ---- return codes ---- */
+#define RYD_OK              0
+#define RYD_ERR_INVALID    -1
+#define RYD_ERR_HIP        -2
+#define RYD_ERR_UNSUPPORTED -3
+#define RYD_ERR_ALLOC      -4
+
+/* ---- protocols (schedules generated on-device from per-point scalars) ---- */
+#define RYD_PROTO_LP_SQUARE 0   /* 2 constant pulses: Omega, Omega*xi      (:693-776)   */
+#define RYD_PROTO_LP_SHAPED 1   /* 2 x (n_steps-1) midpoint segments        (:2099-2231) */
+#define RYD_PROTO_BANGBANG  2   /* <= 8 constant-phase segments, Delta = 0  (:1795-1943) */
+#define RYD_PROTO_SMOOTH_JP 3   /* n_steps midpoint-phase segments          (:1502-1760) */
+
+#define RYD_EVOL_LINDBLAD 0     /* rho (c_ops present)                                   */
+#define RYD_EVOL_KET      1     /* Schrodinger (include_noise=False -> kets, :683-690)    */
+
+#define RYD_METHOD_CHEBYSHEV 0  /* exact-to-1e-14 Chebyshev propagator per segment       */
+#define RYD_METHOD_DOPRI5    1  /* adaptive Dormand-Prince 5(4) (reference-style stepper) */
+
+#define RYD_SHAPE_SQUARE   0
+#define RYD_SHAPE_GAUSSIAN 1
+#define RYD_SHAPE_COSINE   2
+#define RYD_SHAPE_BLACKMAN 3
+
+#define RYD_FLAG_SYMMETRIC_ATOMS 1u  /* atom-B rate columns equal atom-A: faster path */
+
+/* ---- per-point parameter columns ---- */
+#define RYD_P_OMEGA      0   /* |Omega| rad/s (two-photon Rabi)                          */
+#define RYD_P_DELTA      1   /* static detuning of the segments: H -= Delta P_r (LP Delta,
+                                smooth-JP two-photon delta; ignored by BANGBANG)         */
+#define RYD_P_V          2   /* blockade V rad/s (H += V P_rr)                           */
+#define RYD_P_DELTA1     3   /* qubit light shift on |1>: delta_zeeman + delta_stark     */
+#define RYD_P_G1_A       4   /* atom A: |1><r| rate                                      */
+#define RYD_P_G0_A       5   /* atom A: |0><r| rate (decay-to-0 + bbr + losses + leakage) */
+#define RYD_P_GPHI_A     6   /* atom A: P_r dephasing                                    */
+#define RYD_P_GSC_A      7   /* atom A: P_1 dephasing (intermediate scattering)          */
+#define RYD_P_G1_B       8
+#define RYD_P_G0_B       9
+#define RYD_P_GPHI_B     10
+#define RYD_P_GSC_B      11
+#define RYD_P_TAU        12  /* LP: single pulse tau; smooth JP: total tau                */
+#define RYD_P_XI_RE      13  /* LP second pulse factor e^{i xi}                           */
+#define RYD_P_XI_IM      14
+#define RYD_P_AREA_CORR  15  /* shaped LP peak scale                                      */
+#define RYD_P_A          16  /* smooth JP amplitude A                                     */
+#define RYD_P_OMEGA_MOD  17  /* smooth JP omega_mod (rad/s)                               */
+#define RYD_P_PHI_OFF    18  /* smooth JP phase offset                                    */
+#define RYD_P_OMEGA_TAU  19  /* bang-bang total pulse area                                */
+#define RYD_P_NSEG       20  /* bang-bang number of segments (<= 8)                       */
+#define RYD_P_SWT0       21  /* bang-bang dimensionless switching times [7]               */
+#define RYD_P_PHI0       28  /* bang-bang segment phases [8]                              */
+#define RYD_NPARAM       36
+
+/* ---- per-point summary columns ---- */
+#define RYD_S_POP0       0   /* <x|rho_x|x> (or |<x|psi_x>|^2), x = 00,01,10,11 (4 cols) */
+#define RYD_S_OV_RE0     4   /* ket: Re <x|psi_x> (4 cols); Lindblad: NaN                 */
+#define RYD_S_OV_IM0     8   /* ket: Im <x|psi_x> (4 cols)                                */
+#define RYD_S_AVG_POP    12  /* mean population fidelity (no phase penalty)              */
+#define RYD_S_CTRL_PHASE 13  /* ket: wrapped phi11-phi01-phi10+phi00                      */
+#define RYD_S_PENALTY    14  /* ket: cos^2(err/2)                                         */
+#define RYD_S_AVG_F      15  /* ket: reference avg fidelity (F11 penalised); Lindblad: =AVG_POP */
+#define RYD_S_NMV_USEFUL 16  /* generator applications needed per input (flop accounting)*/
+#define RYD_S_NMV_EXEC   17  /* generator applications executed per input (wave-uniform)  */
+#define RYD_S_TRACE11    18  /* Tr rho_11 (Lindblad sanity), ket: |psi_11|^2              */
+#define RYD_NSUMMARY     19
+
+/* ---- per-point status bits ---- */
+#define RYD_STATUS_NONFINITE   1u
+#define RYD_STATUS_STEP_CAP    2u   /* DOPRI5 step cap (ZVODE nsteps analogue)          */
+#define RYD_STATUS_BAD_INPUT   4u   /* Omega <= 0, tau <= 0, nseg out of range ...      */
+
+typedef struct ryd_batch_desc {
+    int32_t abi_version;     /* = RYD_ABI_VERSION */
+    int32_t dim;             /* single-atom levels: 3 */
+    int32_t protocol;        /* RYD_PROTO_* */
+    int32_t evolution;       /* RYD_EVOL_* */
+    int32_t method;          /* RYD_METHOD_* */
+    int32_t shape;           /* RYD_SHAPE_* (LP_SHAPED) */
+    int32_t n_steps;         /* SMOOTH_JP segments (ref 300), LP_SHAPED n_time_steps (ref 500),
+                                BANGBANG: max segments in the batch */
+    uint32_t flags;          /* RYD_FLAG_* */
+    double rtol;             /* DOPRI5 */
+    double atol;             /* DOPRI5 */
+    int64_t max_steps;       /* DOPRI5 step cap per segment */
+} ryd_batch_desc;
+
+typedef struct ryd_stats {
+    double kernel_ms;        /* device time of the propagation kernel(s) */
+    double h2d_ms;
+    double d2h_ms;
+    double matvec_useful;    /* sum over points of 4*RYD_S_NMV_USEFUL */
+    double matvec_exec;
+    int32_t n_devices;
+    int32_t reserved;
+} ryd_stats;
+
+typedef struct ryd_handle ryd_handle;
+
+int         ryd_abi_version(void);
+const char* ryd_last_error(void);
+int         ryd_param_count(void);
+int         ryd_summary_width(void);
+int         ryd_state_width(int evolution, int dim);
+int         ryd_device_count(int* count);
+
+int ryd_create(const int* device_ids, int n_devices, ryd_handle** out);
+int ryd_destroy(ryd_handle* h);
+
+/* Host buffers in/out; range-partitions the points over the handle's devices
+ * (one stream each, no inter-device communication), blocks until done. */
+int ryd_run_batch(ryd_handle* h, const ryd_batch_desc* desc,
+                  const double* params, int64_t n, int64_t ld_params,
+                  double* out_state, int64_t ld_state,
+                  double* out_summary, int64_t ld_summary,
+                  uint32_t* out_status, ryd_stats* stats);
+
+/* Device buffers already resident on device slot `slot`; enqueues on `stream`
+ * (hipStream_t, NULL = the handle's stream for that slot) and returns.
+ * If `elapsed_ms` is non-NULL the call records HIP events around the launch on
+ * that stream, waits, and reports the kernel's device time. */
+int ryd_run_batch_device(ryd_handle* h, int slot, const ryd_batch_desc* desc,
+                         const double* d_params, int64_t n, int64_t ld_params,
+                         double* d_state, int64_t ld_state,
+                         double* d_summary, int64_t ld_summary,
+                         uint32_t* d_status, void* stream, float* elapsed_ms);
+
+/* Minimal device-memory plumbing so callers need no other GPU runtime. */
+int ryd_malloc(ryd_handle* h, int slot, size_t bytes, void** d_ptr);
+int ryd_free(ryd_handle* h, int slot, void* d_ptr);
+int ryd_memcpy_h2d(ryd_handle* h, int slot, void* d_dst, const void* src, size_t bytes);
+int ryd_memcpy_d2h(ryd_handle* h, int slot, void* dst, const void* d_src, size_t bytes);
+int ryd_synchronize(ryd_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RYD_ENGINE_H */

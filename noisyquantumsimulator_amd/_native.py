@@ -1,0 +1,103 @@
+"""ctypes binding of libryd_engine.so (include/ryd_engine.h).
+
+The product path has no CPU fallback: if the in-tree HIP library is missing,
+or no GPU is visible when a batch is run, these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libryd_engine.so")
+
+# keep in sync with include/ryd_engine.h
+RYD_ABI_VERSION = 1
+RYD_OK = 0
+PROTO = {"lp_square": 0, "lp_shaped": 1, "bangbang": 2, "smooth_jp": 3}
+EVOL = {"lindblad": 0, "ket": 1}
+METHOD = {"chebyshev": 0, "dopri5": 1}
+SHAPE = {"square": 0, "gaussian": 1, "cosine": 2, "blackman": 3}
+FLAG_SYMMETRIC_ATOMS = 1
+
+P = dict(OMEGA=0, DELTA=1, V=2, DELTA1=3, G1_A=4, G0_A=5, GPHI_A=6, GSC_A=7, G1_B=8, G0_B=9,
+         GPHI_B=10, GSC_B=11, TAU=12, XI_RE=13, XI_IM=14, AREA_CORR=15, A=16, OMEGA_MOD=17,
+         PHI_OFF=18, OMEGA_TAU=19, NSEG=20, SWT0=21, PHI0=28)
+NPARAM = 36
+S = dict(POP0=0, OV_RE0=4, OV_IM0=8, AVG_POP=12, CTRL_PHASE=13, PENALTY=14, AVG_F=15,
+         NMV_USEFUL=16, NMV_EXEC=17, TRACE11=18)
+NSUMMARY = 19
+STATUS_NONFINITE, STATUS_STEP_CAP, STATUS_BAD_INPUT = 1, 2, 4
+STATE_WIDTH = {"lindblad": 25, "ket": 18}
+
+EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary_width",
+            "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",
+            "ryd_run_batch_device", "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h",
+            "ryd_synchronize")
+
+
+class BatchDesc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("dim", ctypes.c_int32),
+                ("protocol", ctypes.c_int32), ("evolution", ctypes.c_int32),
+                ("method", ctypes.c_int32), ("shape", ctypes.c_int32),
+                ("n_steps", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("rtol", ctypes.c_double), ("atol", ctypes.c_double),
+                ("max_steps", ctypes.c_int64)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("kernel_ms", ctypes.c_double), ("h2d_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double), ("matvec_useful", ctypes.c_double),
+                ("matvec_exec", ctypes.c_double), ("n_devices", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree HIP library (fails loudly if it was not built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(f"{LIB_PATH} is missing: build it with `make` or "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, i64, dp = ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)
+        lib.ryd_abi_version.restype = ctypes.c_int
+        lib.ryd_last_error.restype = ctypes.c_char_p
+        lib.ryd_param_count.restype = ctypes.c_int
+        lib.ryd_summary_width.restype = ctypes.c_int
+        lib.ryd_state_width.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.ryd_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        lib.ryd_create.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(vp)]
+        lib.ryd_destroy.argtypes = [vp]
+        lib.ryd_run_batch.argtypes = [vp, ctypes.POINTER(BatchDesc), dp, i64, i64, dp, i64, dp, i64,
+                                      ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(Stats)]
+        lib.ryd_run_batch_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(BatchDesc), vp, i64, i64,
+                                             vp, i64, vp, i64, vp, vp, ctypes.POINTER(ctypes.c_float)]
+        lib.ryd_malloc.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]
+        lib.ryd_free.argtypes = [vp, ctypes.c_int, vp]
+        lib.ryd_memcpy_h2d.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]
+        lib.ryd_memcpy_d2h.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]
+        lib.ryd_synchronize.argtypes = [vp]
+        if lib.ryd_abi_version() != RYD_ABI_VERSION:
+            raise EngineError("libryd_engine.so ABI version mismatch; rebuild it")
+        if lib.ryd_param_count() != NPARAM or lib.ryd_summary_width() != NSUMMARY:
+            raise EngineError("libryd_engine.so layout mismatch; rebuild it")
+        _lib = lib
+        return lib
+
+
+def check(rc: int) -> None:
+    if rc != RYD_OK:
+        msg = load().ryd_last_error().decode(errors="replace")
+        raise EngineError(f"ryd_engine error {rc}: {msg}")

@@ -1,0 +1,98 @@
+"""Batched sweep drivers (replacing the serial loops of
+examples/research_parameter_sweeps.py:81-195 and the per-point optimizer calls).
+
+Also defines the synthetic benchmark workloads of SURVEY.md §8d.
+"""
+from __future__ import annotations
+
+import warnings
+from typing import Optional
+
+import numpy as np
+
+from . import configurations as CF
+from . import physics as PH
+
+# cz_gate_optimization_demo.ipynb ApparatusConstraints "medium" tier
+MEDIUM = dict(laser_1_power=50e-6, laser_1_waist=50e-6, laser_2_power=0.3, laser_2_waist=50e-6,
+              temperature=2e-6, spacing_factor=2.8, n_rydberg=70, species="Rb87",
+              tweezer_power=0.020, tweezer_waist=0.8e-6, B_field=1e-4, NA=0.5)
+
+
+def medium_excitation(purity: float = 0.99) -> CF.TwoPhotonExcitationConfig:
+    return CF.TwoPhotonExcitationConfig(
+        laser_1=CF.LaserParameters(power=MEDIUM["laser_1_power"], waist=MEDIUM["laser_1_waist"],
+                                   polarization="pi", polarization_purity=purity, linewidth_hz=100.0),
+        laser_2=CF.LaserParameters(power=MEDIUM["laser_2_power"], waist=MEDIUM["laser_2_waist"],
+                                   polarization="sigma+", polarization_purity=purity, linewidth_hz=100.0),
+        Delta_e=2 * np.pi * 1e9)
+
+
+def _apparatus_kwargs(**over):
+    kw = dict(species=MEDIUM["species"], n_rydberg=MEDIUM["n_rydberg"],
+              tweezer_power=MEDIUM["tweezer_power"], tweezer_waist=MEDIUM["tweezer_waist"],
+              temperature=MEDIUM["temperature"], spacing_factor=MEDIUM["spacing_factor"],
+              B_field=MEDIUM["B_field"], NA=MEDIUM["NA"])
+    kw.update(over)
+    return kw
+
+
+def omega_delta_grid(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.0),
+                     delta_over_omega=(0.30, 0.45), omega_tau: float = 4.29268,
+                     include_noise: bool = True, delta_slice: Optional[slice] = None) -> PH.DerivedBatch:
+    """C2: (Omega, Delta) sweep of the LP square CZ gate on the medium apparatus.
+
+    Omega/2pi = linspace(1, 10) MHz is produced the physical way, by scaling the
+    480 nm leg power (Omega ∝ sqrt(P2)); Delta/Omega = linspace(0.30, 0.45);
+    Omega*tau = 4.29268; V = C6/R^6 = 2pi x 1233.83 MHz; every noise rate from the
+    reference formulas per point."""
+    warnings.simplefilter("ignore")
+    exc = medium_excitation()
+    ref = PH.derive_batch(CF.LPSimulationInputs(excitation=exc), **_apparatus_kwargs(),
+                          include_noise=False)
+    om0 = ref["Omega"][0]
+    om = 2 * np.pi * 1e6 * np.linspace(*omega_mhz, n_omega)
+    dom = np.linspace(*delta_over_omega, n_delta)
+    if delta_slice is not None:
+        dom = dom[delta_slice]
+    OM, DOM = np.meshgrid(om, dom, indexing="ij")
+    p2 = MEDIUM["laser_2_power"] * (OM.ravel() / om0) ** 2
+    si = CF.LPSimulationInputs(excitation=exc, omega_tau=omega_tau)
+    return PH.derive_batch(si, n=p2.size, **_apparatus_kwargs(), include_noise=include_noise,
+                           overrides=dict(laser_2_power=p2, delta_over_omega=DOM.ravel()))
+
+
+def pareto_tgate_grid(n_omega: int = 1000, n_tau: int = 100, include_noise: bool = True
+                      ) -> PH.DerivedBatch:
+    """C3: smooth-JP fidelity vs t_gate: Omega/2pi in linspace(1,10) MHz x Omega*tau in
+    linspace(5, 25), medium apparatus (reference noise model)."""
+    warnings.simplefilter("ignore")
+    exc = medium_excitation()
+    ref = PH.derive_batch(CF.SmoothJPSimulationInputs(excitation=exc), **_apparatus_kwargs(),
+                          include_noise=False)
+    om0 = ref["Omega"][0]
+    om = 2 * np.pi * 1e6 * np.linspace(1, 10, n_omega)
+    ot = np.linspace(5, 25, n_tau)
+    OM, OT = np.meshgrid(om, ot, indexing="ij")
+    p2 = MEDIUM["laser_2_power"] * (OM.ravel() / om0) ** 2
+    return PH.derive_batch(CF.SmoothJPSimulationInputs(excitation=exc), n=p2.size,
+                           **_apparatus_kwargs(), include_noise=include_noise,
+                           overrides=dict(laser_2_power=p2, omega_tau=OT.ravel()))
+
+
+def species_temperature_power_grid(n_T: int = 1000, n_P: int = 500, include_noise: bool = True,
+                                   point_slice: Optional[slice] = None) -> PH.DerivedBatch:
+    """C4: species {Rb87, Cs133} x T in logspace(1, 100) uK x P_tweezer in logspace(1, 100) mW,
+    LP square, medium apparatus otherwise.  ``point_slice`` selects a contiguous range
+    shard (multi-GPU range partition) before derivation."""
+    warnings.simplefilter("ignore")
+    sp = np.array(["Rb87", "Cs133"])
+    T = np.logspace(-6, -4, n_T)
+    P = np.logspace(-3, -1, n_P)
+    S_, T_, P_ = np.meshgrid(np.arange(2), T, P, indexing="ij")
+    S_, T_, P_ = S_.ravel(), T_.ravel(), P_.ravel()
+    if point_slice is not None:
+        S_, T_, P_ = S_[point_slice], T_[point_slice], P_[point_slice]
+    return PH.derive_batch(CF.LPSimulationInputs(excitation=medium_excitation()), n=T_.size,
+                           **_apparatus_kwargs(species=sp[S_], temperature=T_, tweezer_power=P_),
+                           include_noise=include_noise)

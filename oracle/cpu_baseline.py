@@ -1,0 +1,61 @@
+"""CPU baseline for bench.py -- TEST/BENCH INFRASTRUCTURE ONLY.
+
+Times the QuTiP-like oracle (ZVODE Adams at the reference tolerances, the
+reference's tlists and per-segment restarts; oracle/lindblad_oracle.py) on a
+bounded sample of the C2 sweep, in a fresh process with single-threaded BLAS
+and a fork pool of worker processes.
+
+    OPENBLAS_NUM_THREADS=1 python -m oracle.cpu_baseline --sample 96 --procs 16
+"""
+import os
+
+# single-threaded BLAS in every worker: set before numpy is imported
+for _v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+    os.environ[_v] = "1"
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import multiprocessing as mp  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+from oracle import lindblad_oracle as O  # noqa: E402
+
+
+def _one(spec):
+    return O.run_point(spec, method="zvode")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sample", type=int, default=96)
+    ap.add_argument("--procs", type=int, default=8)
+    a = ap.parse_args()
+    from noisyquantumsimulator_amd import sweeps as SW
+    b = SW.omega_delta_grid()
+    c = b.cols
+    idx = np.linspace(0, b.n - 1, a.sample).astype(int)
+    specs = [O.PointSpec(protocol="lp_square", Omega=c["Omega"][i], V=c["V"][i],
+                         Delta=c["Delta_gate"][i], tau=c["tau_single"][i],
+                         xi=complex(c["xi_re"][i], c["xi_im"][i]),
+                         delta_zeeman=c["delta_zeeman"][i], delta_stark=c["delta_stark"][i],
+                         c_ops=O.collapse_operators({k: c[k][i] for k in O.RATE_KEYS}))
+             for i in idx]
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(a.procs) as pool:
+        pool.map(_one, specs, chunksize=1)
+    wall = time.perf_counter() - t0
+    print(json.dumps(dict(
+        value=a.sample / wall, unit="points/s", cores=a.procs, kind="port",
+        sample=f"{a.sample} points evenly spaced over the C2 10k sweep; oracle ZVODE-Adams "
+               f"restatement of qutip.mesolve (atol 1e-10, rtol 1e-8, reference tlists); "
+               f"{a.procs} single-threaded worker processes; {wall:.2f} s wall")))
+
+
+if __name__ == "__main__":
+    main()

@@ -19,6 +19,11 @@ Nothing here is shipped; the GPU box only sees the JSON fixtures.
 """
 from __future__ import annotations
 
+import os
+
+for _v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+    os.environ.setdefault(_v, "1")
+
 import importlib.util
 import json
 import os

@@ -1,0 +1,47 @@
+"""CPU-side checks of the C-ABI library: it loads and exports every symbol
+include/ryd_engine.h declares, with matching layout constants.  No compute."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from noisyquantumsimulator_amd import _native as N
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header():
+    with open(os.path.join(REPO, "include", "ryd_engine.h")) as f:
+        return f.read()
+
+
+def test_header_declares_exported_symbols():
+    decl = set(re.findall(r"\b(ryd_[a-z0-9_]+)\s*\(", _header()))
+    assert decl == set(N.EXPORTED)
+
+
+def test_header_constants_match_binding():
+    h = _header()
+    defs = dict(re.findall(r"#define\s+(RYD_[A-Z0-9_]+)\s+(-?\d+)u?", h))
+    for k, v in N.P.items():
+        assert int(defs["RYD_P_" + k]) == v
+    for k, v in N.S.items():
+        assert int(defs["RYD_S_" + k]) == v
+    assert int(defs["RYD_NPARAM"]) == N.NPARAM and int(defs["RYD_NSUMMARY"]) == N.NSUMMARY
+    for k, v in N.PROTO.items():
+        assert int(defs["RYD_PROTO_" + k.upper()]) == v
+    assert ctypes.sizeof(N.BatchDesc) == 56 and ctypes.sizeof(N.Stats) == 48
+
+
+def test_library_loads_and_exports():
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("libryd_engine.so not built (run make / __graft_entry__.build())")
+    lib = N.load()
+    for sym in N.EXPORTED:
+        assert hasattr(lib, sym), sym
+    assert lib.ryd_abi_version() == 1
+    assert lib.ryd_param_count() == N.NPARAM
+    assert lib.ryd_summary_width() == N.NSUMMARY
+    assert lib.ryd_state_width(0, 3) == 25 and lib.ryd_state_width(1, 3) == 18
+    assert lib.ryd_state_width(0, 4) == -1
