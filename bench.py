@@ -25,8 +25,10 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (spec)
-# FLOPs per generator application per lane: apply_A 75 + apply_B 75 + V 12 + Clenshaw 25 FMAs
+# FLOPs per generator application (one 25-vector): apply_A 75 + apply_B 75 + V 12 + Clenshaw 25 FMAs
 FLOP_PER_MATVEC = 2 * (75 + 75 + 12 + 25)
+FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
+FLOP_PER_STATE_UPDATE = 2 * 4 * 25 ** 2  # R_k <- U R_k for the 4 inputs, per segment
 N_OMEGA, N_DELTA = 100, 100
 
 
@@ -74,6 +76,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64)
+    ap.add_argument("--method", default="chebyshev",
+                    choices=["chebyshev", "cheb_squaring", "cheb_vector"])
     args = ap.parse_args()
 
     ws, rank, local, pg = _dist()
@@ -87,7 +91,7 @@ def main():
     params = E.pack_params(batch)
     n = batch.n
     eng = E.Engine(devices=[local])
-    db = E.DeviceBatch(eng, params, "lp_square", "lindblad")
+    db = E.DeviceBatch(eng, params, "lp_square", "lindblad", method=args.method)
 
     for _ in range(args.warmup):
         db.launch()
@@ -111,7 +115,10 @@ def main():
     # + 1 status word written per point
     bytes_per_point = 8 * 15 + 8 * 100 + 8 * 19 + 4
     achieved_gbs = bytes_per_point * n / (k_ms * 1e-3) / 1e9
-    flops = res.matvec_useful * FLOP_PER_MATVEC
+    nsq = float(res.col("NSQUARE").sum())
+    flops = res.matvec_useful * FLOP_PER_MATVEC + nsq * FLOP_PER_SQUARING
+    if nsq > 0:
+        flops += 2 * n * FLOP_PER_STATE_UPDATE          # 2 segments per LP-square point
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
 
     total_points = n * ws * args.steps
@@ -125,7 +132,8 @@ def main():
         "config": {"workload": "C2: 10k-point (Omega, Delta) LP-square CZ sweep per GPU, "
                                "medium apparatus, full reference noise model (8 Lindblad channels)",
                    "points_per_gpu": n, "global_points": n * ws, "parallelism": f"range-shard x{ws}",
-                   "method": "chebyshev"},
+                   "method": args.method + (" (auto: propagator squaring for LP square)"
+                                            if args.method == "chebyshev" else "")},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
                      "kernel_ms": k_ms, "bytes_per_launch": bytes_per_point * n},

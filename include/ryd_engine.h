@@ -66,8 +66,12 @@ extern "C" {
 #define RYD_EVOL_LINDBLAD 0     /* rho (c_ops present)                                   */
 #define RYD_EVOL_KET      1     /* Schrodinger (include_noise=False -> kets, :683-690)    */
 
-#define RYD_METHOD_CHEBYSHEV 0  /* exact-to-1e-14 Chebyshev propagator per segment       */
-#define RYD_METHOD_DOPRI5    1  /* adaptive Dormand-Prince 5(4) (reference-style stepper) */
+#define RYD_METHOD_CHEBYSHEV      0  /* auto: squaring for few long segments (LP square,
+                                         bang-bang, Lindblad), vector otherwise            */
+#define RYD_METHOD_DOPRI5         1  /* adaptive Dormand-Prince 5(4) (reference-style stepper) */
+#define RYD_METHOD_CHEB_VECTOR    2  /* Chebyshev on the 4 input states, one lane each      */
+#define RYD_METHOD_CHEB_SQUARING  3  /* Chebyshev on 25 basis columns of exp(L dt/2^s),
+                                         then s squarings in LDS (Lindblad only)            */
 
 #define RYD_SHAPE_SQUARE   0
 #define RYD_SHAPE_GAUSSIAN 1
@@ -111,10 +115,11 @@ extern "C" {
 #define RYD_S_CTRL_PHASE 13  /* ket: wrapped phi11-phi01-phi10+phi00                      */
 #define RYD_S_PENALTY    14  /* ket: cos^2(err/2)                                         */
 #define RYD_S_AVG_F      15  /* ket: reference avg fidelity (F11 penalised); Lindblad: =AVG_POP */
-#define RYD_S_NMV_USEFUL 16  /* generator applications needed per input (flop accounting)*/
-#define RYD_S_NMV_EXEC   17  /* generator applications executed per input (wave-uniform)  */
+#define RYD_S_NMV_USEFUL 16  /* generator applications needed, whole point (flop accounting) */
+#define RYD_S_NMV_EXEC   17  /* generator applications executed, whole point (wave-uniform)  */
 #define RYD_S_TRACE11    18  /* Tr rho_11 (Lindblad sanity), ket: |psi_11|^2              */
-#define RYD_NSUMMARY     19
+#define RYD_S_NSQUARE    19  /* 25x25 squarings performed (squaring method)               */
+#define RYD_NSUMMARY     20
 
 /* ---- per-point status bits ---- */
 #define RYD_STATUS_NONFINITE   1u
@@ -140,7 +145,7 @@ typedef struct ryd_stats {
     double kernel_ms;        /* device time of the propagation kernel(s) */
     double h2d_ms;
     double d2h_ms;
-    double matvec_useful;    /* sum over points of 4*RYD_S_NMV_USEFUL */
+    double matvec_useful;    /* sum over points of RYD_S_NMV_USEFUL */
     double matvec_exec;
     int32_t n_devices;
     int32_t reserved;

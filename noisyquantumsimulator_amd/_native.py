@@ -17,7 +17,7 @@ RYD_ABI_VERSION = 1
 RYD_OK = 0
 PROTO = {"lp_square": 0, "lp_shaped": 1, "bangbang": 2, "smooth_jp": 3}
 EVOL = {"lindblad": 0, "ket": 1}
-METHOD = {"chebyshev": 0, "dopri5": 1}
+METHOD = {"chebyshev": 0, "dopri5": 1, "cheb_vector": 2, "cheb_squaring": 3}
 SHAPE = {"square": 0, "gaussian": 1, "cosine": 2, "blackman": 3}
 FLAG_SYMMETRIC_ATOMS = 1
 
@@ -26,8 +26,8 @@ P = dict(OMEGA=0, DELTA=1, V=2, DELTA1=3, G1_A=4, G0_A=5, GPHI_A=6, GSC_A=7, G1_
          PHI_OFF=18, OMEGA_TAU=19, NSEG=20, SWT0=21, PHI0=28)
 NPARAM = 36
 S = dict(POP0=0, OV_RE0=4, OV_IM0=8, AVG_POP=12, CTRL_PHASE=13, PENALTY=14, AVG_F=15,
-         NMV_USEFUL=16, NMV_EXEC=17, TRACE11=18)
-NSUMMARY = 19
+         NMV_USEFUL=16, NMV_EXEC=17, TRACE11=18, NSQUARE=19)
+NSUMMARY = 20
 STATUS_NONFINITE, STATUS_STEP_CAP, STATUS_BAD_INPUT = 1, 2, 4
 STATE_WIDTH = {"lindblad": 25, "ket": 18}
 

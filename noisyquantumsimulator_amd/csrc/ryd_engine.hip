@@ -488,9 +488,10 @@ __global__ __launch_bounds__(BLOCK) void lindblad_cheb_kernel(
     sm[(int64_t)RYD_S_CTRL_PHASE * ldm + i] = nan;
     sm[(int64_t)RYD_S_PENALTY * ldm + i] = nan;
     sm[(int64_t)RYD_S_AVG_F * ldm + i] = avg;
-    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = nuse;
-    sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = nexec;
+    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = 4.0 * nuse;   // 4 basis-input lanes per point
+    sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = 4.0 * nexec;
     sm[(int64_t)RYD_S_TRACE11 * ldm + i] = tr11;
+    sm[(int64_t)RYD_S_NSQUARE * ldm + i] = 0.0;
     status[i] = st_all;
   }
 }
@@ -593,10 +594,190 @@ __global__ __launch_bounds__(BLOCK) void ket_cheb_kernel(
     sm[(int64_t)RYD_S_CTRL_PHASE * ldm + i] = cp;
     sm[(int64_t)RYD_S_PENALTY * ldm + i] = pen;
     sm[(int64_t)RYD_S_AVG_F * ldm + i] = avgf;
-    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = nuse;
-    sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = nexec;
+    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = 4.0 * nuse;
+    sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = 4.0 * nexec;
     sm[(int64_t)RYD_S_TRACE11 * ldm + i] = nrm11;
+    sm[(int64_t)RYD_S_NSQUARE * ldm + i] = 0.0;
     status[i] = st_all;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Propagator-squaring kernel (few long constant segments: LP square, bang-bang)
+// ---------------------------------------------------------------------------
+// Per segment and point: U = exp(L dt) on the 25-dim sector, built as
+//   (1) U0 = exp(L dt / 2^s): one basis column per lane (25 lanes per point),
+//       the same Chebyshev/Miller Clenshaw loop as above on x/2^s <= X_BASE;
+//   (2) s squarings U <- U U in LDS; each lane owns a 5x5 output tile
+//       (point p, row block rb, col block cb), 625 FMAs and ~200 LDS reads per
+//       squaring;
+//   (3) R_k <- U R_k for the 4 basis-input states (kept in LDS).
+// Work per segment is O(log x) instead of O(x): the x = 5000 segments of the
+// Omega/2pi = 1 MHz points cost ~12x less, and every point costs about the same,
+// which removes the launch's critical-path imbalance.
+constexpr int PPB = 10;                     // points per 256-lane block (250 lanes used)
+constexpr int NC = 25;
+constexpr double X_BASE = 6.0;              // Chebyshev argument after scaling
+
+template <int PROTO, bool SYM>
+__global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
+    const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ st, int64_t lds,
+    double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
+  __shared__ __attribute__((aligned(16))) double U[PPB][NC][NC];    // row-major U[p][row][col]
+  __shared__ __attribute__((aligned(16))) double Rs[PPB][4][NC];    // basis-input states
+  __shared__ int s_max;
+
+  const int t = threadIdx.x;
+  const bool lane_ok = t < PPB * NC;
+  const int pl = lane_ok ? t / NC : 0;     // point within block
+  const int j = t % NC;                    // column (phase 1) / tile id (phase 2)
+  const int64_t ip = (int64_t)blockIdx.x * PPB + pl;
+  const bool live = lane_ok && ip < n;
+  const int64_t i = ip < n ? ip : n - 1;
+  const bool valid = point_valid<PROTO>(load_point<PROTO>(prm, ldp, i), n_steps);
+  const int rb = j / 5, cb = j % 5;        // 5x5 tile of the point's 25x25 product
+
+  for (int e = t; e < PPB * 4 * NC; e += BLOCK) {
+    const int p = e / (4 * NC), k = (e / NC) % 4, r = e % NC;
+    const int e0 = 5 * (k >> 1) + (k & 1);
+    Rs[p][k][r] = (r == e0) ? 1.0 : 0.0;
+  }
+  double nuse = 0.0, nexec = 0.0, nsq = 0.0;
+  bool over_cap = false;
+  const int nseg = n_segments<PROTO>(n_steps);
+
+  for (int s = 0; s < nseg; ++s) {
+    // re-read this point's scalars every segment (L1/L2 hits) instead of keeping
+    // them live across the loop: the Chebyshev phase needs the VGPRs
+    const double* pp = prm;
+    asm volatile("" : "+s"(pp));
+    const PointP q = load_point<PROTO>(pp, ldp, i);
+    double rsum = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) rsum += fabs(q.gA[c]) + fabs(q.gB[c]);
+    const Seg g = segment<PROTO>(q, s, n_steps, shape);
+    double emin, emax;
+    h_bounds(g, q.V, q.d1, emin, emax);
+    const double omega = (emax - emin) + rsum;
+    const double x = omega * g.dt;
+    const bool capped = valid && !(x <= 1e12);
+    const bool active = valid && !capped && x > X_SKIP && lane_ok;
+    over_cap = over_cap || capped;
+    int sq = 0;
+    if (active && x > X_BASE) sq = (int)ceil(log2(x / X_BASE));
+    const double y = active ? ldexp(x, -sq) : 0.0;
+    const double sc = active ? 2.0 / omega : 0.0;
+    const Gen A = make_gen(g, q.d1, q.gA, sc);
+    const Gen B = make_gen(g, q.d1, q.gB, sc);
+    const double vs = sc * 0.5 * q.V;
+    // (1) column j of exp(y Y)
+    double v[25];
+#pragma unroll
+    for (int e = 0; e < 25; ++e) v[e] = (e == j) ? 1.0 : 0.0;
+    cheb_segment<25>(v, y, active,
+                     [&](const double (&b)[25], double (&o)[25]) { apply_L<SYM>(A, B, vs, b, o); },
+                     nuse, nexec);
+    if (t == 0) s_max = 0;
+    __syncthreads();
+    if (lane_ok) {
+#pragma unroll
+      for (int r = 0; r < 25; ++r) {
+        U[pl][r][j] = v[r];
+      }
+      atomicMax(&s_max, sq);
+    }
+    __syncthreads();
+    const int smx = s_max;
+    nsq += (double)sq;
+    // (2) squarings: tile (rb, cb) of U U
+    for (int it = 0; it < smx; ++it) {
+      double acc[5][5];
+#pragma unroll
+      for (int a = 0; a < 5; ++a)
+#pragma unroll
+        for (int b = 0; b < 5; ++b) acc[a][b] = 0.0;
+      if (lane_ok && it < sq) {
+        for (int k = 0; k < NC; ++k) {
+          double ar[5], bc[5];
+#pragma unroll
+          for (int a = 0; a < 5; ++a) ar[a] = U[pl][5 * rb + a][k];
+#pragma unroll
+          for (int b = 0; b < 5; ++b) bc[b] = U[pl][k][5 * cb + b];    // U[k][5cb+b]
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int b = 0; b < 5; ++b) acc[a][b] = fma(ar[a], bc[b], acc[a][b]);
+        }
+      }
+      __syncthreads();
+      if (lane_ok && it < sq) {
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+#pragma unroll
+          for (int b = 0; b < 5; ++b) {
+            U[pl][5 * rb + a][5 * cb + b] = acc[a][b];
+          }
+      }
+      __syncthreads();
+    }
+    // (3) R_k <- U R_k ; lane (pl, r = j) computes row r for the 4 inputs
+    double nr[4] = {0.0, 0.0, 0.0, 0.0};
+    if (lane_ok) {
+      for (int m = 0; m < NC; ++m) {
+        const double u = U[pl][j][m];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nr[k] = fma(u, Rs[pl][k][m], nr[k]);
+      }
+    }
+    __syncthreads();
+    if (lane_ok) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
+    }
+    __syncthreads();
+  }
+
+  // outputs: state rows st[e][4*i + k] (staged through LDS, coalesced over 40 lanes/row)
+  const int64_t i0 = (int64_t)blockIdx.x * PPB;
+  for (int e = t; e < NC * PPB * 4; e += BLOCK) {
+    const int r = e / (PPB * 4), c = e % (PPB * 4);
+    const int p = c / 4, k = c % 4;
+    if (i0 + p < n) st[(int64_t)r * lds + 4 * i0 + c] = Rs[p][k][r];
+  }
+  uint32_t stat = valid ? 0u : RYD_STATUS_BAD_INPUT;
+  if (over_cap) stat |= RYD_STATUS_STEP_CAP;
+  if (live && j == 0) {
+    double pops[4], tr11 = 0.0;
+    bool fin = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e0 = 5 * (k >> 1) + (k & 1);
+      pops[k] = Rs[pl][k][e0];
+    }
+    for (int r = 0; r < NC; ++r)
+      for (int k = 0; k < 4; ++k) fin = fin && isfinite(Rs[pl][k][r]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) tr11 += Rs[pl][3][5 * a + b];
+    if (!fin) stat |= RYD_STATUS_NONFINITE;
+    const double nan = __builtin_nan("");
+    const double avg = 0.25 * (pops[0] + pops[1] + pops[2] + pops[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sm[(int64_t)(RYD_S_POP0 + k) * ldm + i] = pops[k];
+      sm[(int64_t)(RYD_S_OV_RE0 + k) * ldm + i] = nan;
+      sm[(int64_t)(RYD_S_OV_IM0 + k) * ldm + i] = nan;
+    }
+    sm[(int64_t)RYD_S_AVG_POP * ldm + i] = avg;
+    sm[(int64_t)RYD_S_CTRL_PHASE * ldm + i] = nan;
+    sm[(int64_t)RYD_S_PENALTY * ldm + i] = nan;
+    sm[(int64_t)RYD_S_AVG_F * ldm + i] = avg;
+    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = NC * nuse;   // 25 basis columns per point
+    sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = NC * nexec;
+    sm[(int64_t)RYD_S_TRACE11 * ldm + i] = tr11;
+    sm[(int64_t)RYD_S_NSQUARE * ldm + i] = nsq;
+    status[i] = stat;
   }
 }
 
@@ -622,6 +803,18 @@ using KernelFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, dou
 
 KernelFn pick_kernel(const ryd_batch_desc* d) {
   const bool sym = (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0;
+  const bool few_long = d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG;
+  const bool squaring = d->method == RYD_METHOD_CHEB_SQUARING ||
+                        (d->method == RYD_METHOD_CHEBYSHEV && few_long);
+  if (d->evolution == RYD_EVOL_LINDBLAD && squaring) {
+    if (d->protocol == RYD_PROTO_LP_SQUARE)
+      return sym ? lindblad_prop_kernel<RYD_PROTO_LP_SQUARE, true> : lindblad_prop_kernel<RYD_PROTO_LP_SQUARE, false>;
+    if (d->protocol == RYD_PROTO_BANGBANG)
+      return sym ? lindblad_prop_kernel<RYD_PROTO_BANGBANG, true> : lindblad_prop_kernel<RYD_PROTO_BANGBANG, false>;
+    if (d->protocol == RYD_PROTO_SMOOTH_JP)
+      return sym ? lindblad_prop_kernel<RYD_PROTO_SMOOTH_JP, true> : lindblad_prop_kernel<RYD_PROTO_SMOOTH_JP, false>;
+    return sym ? lindblad_prop_kernel<RYD_PROTO_LP_SHAPED, true> : lindblad_prop_kernel<RYD_PROTO_LP_SHAPED, false>;
+  }
   if (d->evolution == RYD_EVOL_LINDBLAD) {
     switch (d->protocol) {
       case RYD_PROTO_LP_SQUARE:
@@ -648,7 +841,11 @@ int validate(const ryd_batch_desc* d, int64_t n, int64_t ldp, int64_t lds, int64
   if (!d) return fail(RYD_ERR_INVALID, "desc is NULL");
   if (d->abi_version != RYD_ABI_VERSION) return fail(RYD_ERR_INVALID, "abi_version mismatch");
   if (d->dim != 3) return fail(RYD_ERR_UNSUPPORTED, "only hilbert_space_dim=3 is implemented");
-  if (d->method != RYD_METHOD_CHEBYSHEV) return fail(RYD_ERR_UNSUPPORTED, "method not implemented");
+  if (d->method != RYD_METHOD_CHEBYSHEV && d->method != RYD_METHOD_CHEB_VECTOR &&
+      d->method != RYD_METHOD_CHEB_SQUARING)
+    return fail(RYD_ERR_UNSUPPORTED, "method not implemented");
+  if (d->method == RYD_METHOD_CHEB_SQUARING && d->evolution != RYD_EVOL_LINDBLAD)
+    return fail(RYD_ERR_UNSUPPORTED, "squaring method is Lindblad-only");
   if (d->protocol < 0 || d->protocol > 3) return fail(RYD_ERR_INVALID, "bad protocol");
   if (d->evolution != RYD_EVOL_LINDBLAD && d->evolution != RYD_EVOL_KET)
     return fail(RYD_ERR_INVALID, "bad evolution");
@@ -668,8 +865,11 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
   if (n == 0) return RYD_OK;
   KernelFn k = pick_kernel(d);
   if (!k) return fail(RYD_ERR_UNSUPPORTED, "no kernel for this descriptor");
-  const int64_t lanes = 4 * n;
-  const int64_t blocks = (lanes + BLOCK - 1) / BLOCK;
+  const bool few_long = d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG;
+  const bool squaring = d->evolution == RYD_EVOL_LINDBLAD &&
+                        (d->method == RYD_METHOD_CHEB_SQUARING ||
+                         (d->method == RYD_METHOD_CHEBYSHEV && few_long));
+  const int64_t blocks = squaring ? (n + PPB - 1) / PPB : (4 * n + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
   int ns = d->n_steps, sh = d->shape;
   void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
@@ -907,8 +1107,8 @@ int ryd_run_batch(ryd_handle* h, const ryd_batch_desc* desc, const double* param
     stats->d2h_ms = dms;
     double u = 0.0, x = 0.0;
     for (int64_t i = 0; i < n; ++i) {
-      u += 4.0 * out_summary[(int64_t)RYD_S_NMV_USEFUL * ld_summary + i];
-      x += 4.0 * out_summary[(int64_t)RYD_S_NMV_EXEC * ld_summary + i];
+      u += out_summary[(int64_t)RYD_S_NMV_USEFUL * ld_summary + i];
+      x += out_summary[(int64_t)RYD_S_NMV_EXEC * ld_summary + i];
     }
     stats->matvec_useful = u;
     stats->matvec_exec = x;

@@ -261,7 +261,7 @@ class DeviceBatch:
         N.check(lib.ryd_memcpy_d2h(h, s, summ.ctypes.data, self.d_summary, summ.nbytes))
         N.check(lib.ryd_memcpy_d2h(h, s, status.ctypes.data, self.d_status, status.nbytes))
         return EngineResult(self.evolution, self.n, state, summ, status, 0.0, 0.0, 0.0,
-                            4 * summ[N.S["NMV_USEFUL"]].sum(), 4 * summ[N.S["NMV_EXEC"]].sum())
+                            summ[N.S["NMV_USEFUL"]].sum(), summ[N.S["NMV_EXEC"]].sum())
 
     def free(self):
         for p in self._bufs:

@@ -1,0 +1,462 @@
+"""simulate_CZ_gate on the MI355X engine -- the drop-in for the reference's
+point-level contract (RG/simulation.py:2534-3676) and its batched form.
+
+``simulate_CZ_gate``        same signature / SimulationResult as the reference;
+                            a batch of one through the engine.
+``simulate_CZ_gate_batch``  the sweep form: any apparatus argument may be an
+                            array; all points go through ONE engine launch per
+                            evolution kind (kets for noise-free points, rho in the
+                            25-dim sector otherwise), then the fidelity epilogue.
+``compute_CZ_fidelity``     RG/simulation.py:225-633 on numpy states.
+
+Fidelity epilogue.  Noise-free (ket) points: everything (populations, overlap
+phases, controlled phase, cos^2 penalty, average) comes from the GPU summary.
+Noisy (rho) points: populations come from the GPU; the reference's controlled
+phase uses the dominant eigenvector of each 9x9 rho (:424-452), whose phase is
+the eigensolver's gauge choice (SURVEY.md §7 hard part 3).  ``phase_penalty``:
+  "reference" (default) -- LAPACK eigh on the host on the full rho, as QuTiP's
+                 Qobj.eigenstates does (scipy.linalg.eigh by default,
+                 ``eigh="numpy"`` for numpy's batched zheevd);
+  "none"       -- gauge-invariant population fidelity only (F11 unpenalised).
+"""
+from __future__ import annotations
+
+import warnings
+from dataclasses import dataclass, field
+from types import SimpleNamespace
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+
+from . import _native as N
+from . import operators as OPS
+from . import physics as PH
+from .configurations import (AtomicConfiguration, JPSimulationInputs, LPSimulationInputs,
+                             SmoothJPSimulationInputs)
+from .constants import KB
+
+LABELS = ("00", "01", "10", "11")
+_IDX = {"00": 0, "01": 1, "10": 3, "11": 4}        # basis index 3*a1 + a2 (dim 3)
+
+
+# ---------------------------------------------------------------------------
+# fidelity (RG/simulation.py:186-633)
+# ---------------------------------------------------------------------------
+
+def _eigh_fn(eigh):
+    if eigh is None or eigh == "scipy":
+        import scipy.linalg as sla
+        return lambda m: sla.eigh(m)
+    if eigh == "numpy":
+        return np.linalg.eigh
+    return eigh
+
+
+def _wrap(cp):
+    return (cp + np.pi) % (2 * np.pi) - np.pi
+
+
+def _penalty(cp):
+    err = np.minimum(np.abs(cp - np.pi), np.abs(cp + np.pi))
+    return err, np.cos(err / 2) ** 2
+
+
+def compute_CZ_fidelity(results: Dict[str, np.ndarray], extract_global_phase: bool = True,
+                        hilbert_space_dim: int = 3, eigh=None) -> Tuple[Dict[str, float], float, Dict]:
+    """Per-state fidelities, average and phase_info, as RG/simulation.py:225-633."""
+    d = hilbert_space_dim
+    idx = {lab: int(np.argmax(np.abs(v))) for lab, v in OPS.basis_kets(d).items()}
+    mixed = np.ndim(results["01"]) == 2
+    phase_info: Dict[str, Any] = {}
+    fid: Dict[str, float] = {}
+    if mixed:
+        pops = {lab: float(np.real(results[lab][idx[lab], idx[lab]])) for lab in LABELS}
+        fid.update(pops)
+        if extract_global_phase:
+            eg = _eigh_fn(eigh)
+            ph = {}
+            for lab in LABELS:
+                try:
+                    w, U = eg(results[lab])
+                    ph[lab] = float(np.angle(U[idx[lab], int(np.argmax(w))]))
+                except Exception:
+                    ph[lab] = 0.0
+            cp = float(_wrap(ph["11"] - ph["01"] - ph["10"] + ph["00"]))
+            err, pen = _penalty(cp)
+            phase_info = {
+                "phi_01_rad": ph["01"], "phi_01_deg": np.degrees(ph["01"]),
+                "phi_11_rad": ph["11"], "phi_11_deg": np.degrees(ph["11"]),
+                "expected_phi_11_rad": -np.pi, "controlled_phase_rad": cp,
+                "controlled_phase_deg": np.degrees(cp), "phase_error_from_pi_rad": float(err),
+                "phase_error_from_pi_deg": float(np.degrees(err)), "cz_phase_fidelity": float(pen),
+                "amp_01": np.sqrt(max(0, pops["01"])), "amp_11": np.sqrt(max(0, pops["11"])),
+                "pop_00": pops["00"], "pop_01": pops["01"], "pop_11": pops["11"],
+                "is_mixed_state": True,
+                "note": "Phase extracted from dominant eigenvector - penalty applied for CZ condition",
+            }
+    else:
+        ov = {lab: complex(results[lab][idx[lab]]) for lab in LABELS}
+        for lab in LABELS:
+            fid[lab] = float(abs(ov[lab]) ** 2)
+        if extract_global_phase:
+            phi01 = float(np.angle(ov["01"]))
+            phi11 = float(np.angle(-ov["11"]))
+            amp11 = abs(ov["11"])
+            perr = float(np.arccos(np.clip(amp11, 0, 1)))
+            cp = float(_wrap(np.angle(ov["11"]) - np.angle(ov["01"]) - np.angle(ov["10"])
+                             + np.angle(ov["00"])))
+            err, pen = _penalty(cp)
+            phase_info = {
+                "phi_01_rad": phi01, "phi_01_deg": np.degrees(phi01),
+                "phi_11_rad": phi11, "phi_11_deg": np.degrees(phi11),
+                "phi_11_plus_rad": float(np.angle(ov["11"])),
+                "phi_11_plus_deg": float(np.degrees(np.angle(ov["11"]))),
+                "phase_error_rad": perr, "phase_error_deg": np.degrees(perr),
+                "amp_01": abs(ov["01"]), "amp_11": amp11, "is_mixed_state": False,
+                "controlled_phase_rad": cp, "controlled_phase_deg": np.degrees(cp),
+                "phase_error_from_pi_rad": float(err), "phase_error_from_pi_deg": float(np.degrees(err)),
+                "cz_phase_fidelity": float(pen),
+            }
+    if phase_info:
+        pen = phase_info.get("cz_phase_fidelity", 1.0)
+        phase_info["F11_population"] = fid["11"]
+        phase_info["F11_with_phase"] = fid["11"] * pen
+        phase_info["cz_phase_condition_met"] = phase_info.get("phase_error_from_pi_rad", 0) < 0.2
+        fid["11"] = fid["11"] * pen
+    return fid, float(np.mean([fid[k] for k in LABELS])), phase_info
+
+
+def mixed_phase_penalty(rho: np.ndarray, eigh=None) -> Tuple[np.ndarray, np.ndarray]:
+    """Vectorised dominant-eigenvector controlled phase for rho[n, 4, 9, 9]
+    -> (controlled_phase[n], penalty[n])."""
+    n = rho.shape[0]
+    ph = np.zeros((n, 4))
+    if eigh == "numpy":
+        w, U = np.linalg.eigh(rho.reshape(-1, 9, 9))
+        k = np.argmax(w, axis=1)
+        vmax = U[np.arange(U.shape[0]), :, k]                    # (4n, 9)
+        comp = np.array([_IDX[l] for l in LABELS] * n)
+        ph = np.angle(vmax[np.arange(4 * n), comp]).reshape(n, 4)
+    else:
+        eg = _eigh_fn(eigh)
+        for i in range(n):
+            for k, lab in enumerate(LABELS):
+                w, U = eg(rho[i, k])
+                ph[i, k] = np.angle(U[_IDX[lab], int(np.argmax(w))])
+    cp = _wrap(ph[:, 3] - ph[:, 1] - ph[:, 2] + ph[:, 0])
+    return cp, _penalty(cp)[1]
+
+
+# ---------------------------------------------------------------------------
+# results
+# ---------------------------------------------------------------------------
+
+@dataclass
+class SimulationResult:
+    """Same fields and properties as RG/simulation.py:2238-2531.  ``results``,
+    ``H1``, ``H2``, ``c_ops`` are numpy arrays (the reference returns qutip.Qobj)."""
+    avg_fidelity: float
+    fidelities: Dict[str, float]
+    phase_info: Dict
+    protocol: str
+    n_pulses: int
+    hilbert_space_dim: int
+    Omega: float
+    V: float
+    Delta: float
+    V_over_Omega: float
+    tau_single: float
+    tau_total: float
+    R: float
+    Delta_over_Omega: float = 0.0
+    xi: complex = 1.0
+    spacing_factor: float = 2.8
+    U0_mK: float = 0.0
+    omega_r_kHz: float = 0.0
+    sigma_r_nm: float = 0.0
+    trap_wavelength_nm: float = 1064.0
+    magic_wavelength_analysis: Dict = None
+    noise_breakdown: Dict = None
+    include_noise: bool = True
+    include_motional_dephasing: bool = True
+    pulse_info: Dict = None
+    config: AtomicConfiguration = None
+    species: str = "Rb87"
+    n_rydberg: int = 70
+    qubit_0: Tuple[int, int] = (1, 0)
+    qubit_1: Tuple[int, int] = (2, 0)
+    temperature_K: float = 2e-6
+    B_field_T: float = 1e-4
+    delta_zeeman: float = 0.0
+    delta_stark: float = 0.0
+    trap_laser_on: bool = True
+    results: Dict = None
+    H1: Any = None
+    H2: Any = None
+    c_ops: List = None
+    hs: Any = None
+
+    def __post_init__(self):
+        for k in ("magic_wavelength_analysis", "noise_breakdown", "pulse_info", "results"):
+            if getattr(self, k) is None:
+                setattr(self, k, {})
+        if self.c_ops is None:
+            self.c_ops = []
+
+    Omega_MHz = property(lambda s: s.Omega / (2 * np.pi * 1e6))
+    V_MHz = property(lambda s: s.V / (2 * np.pi * 1e6))
+    Delta_MHz = property(lambda s: s.Delta / (2 * np.pi * 1e6))
+    gate_time_us = property(lambda s: s.tau_total * 1e6)
+    R_um = property(lambda s: s.R * 1e6)
+    xi_rad = property(lambda s: float(np.angle(s.xi)))
+    xi_deg = property(lambda s: float(np.degrees(np.angle(s.xi))))
+    temperature_uK = property(lambda s: s.temperature_K * 1e6)
+    B_field_Gauss = property(lambda s: s.B_field_T * 1e4)
+
+    def print_summary(self):
+        print("=" * 70)
+        print("CZ GATE SIMULATION RESULTS")
+        print("=" * 70)
+        print(f"Average fidelity: {self.avg_fidelity:.6f} ({(1 - self.avg_fidelity) * 100:.4f}% error)")
+        for state, f in self.fidelities.items():
+            print(f"  |{state}⟩ → {f:.6f}")
+        print(f"Protocol: {self.protocol}   pulses: {self.n_pulses}   dim: {self.hilbert_space_dim}")
+        print(f"Ω/(2π): {self.Omega_MHz:.3f} MHz   V/(2π): {self.V_MHz:.2f} MHz   V/Ω: {self.V_over_Omega:.2f}")
+        print(f"Total gate: {self.gate_time_us:.3f} μs   R: {self.R_um:.2f} μm   U0: {self.U0_mK:.2f} mK")
+        print("=" * 70)
+
+
+@dataclass
+class BatchResult:
+    """SoA outputs of simulate_CZ_gate_batch (one row per point)."""
+    batch: PH.DerivedBatch
+    avg_fidelity: np.ndarray
+    fidelities: np.ndarray            # (n, 4): F00, F01, F10, F11 (F11 penalised)
+    populations: np.ndarray           # (n, 4)
+    controlled_phase: np.ndarray
+    cz_phase_fidelity: np.ndarray
+    status: np.ndarray
+    is_mixed: np.ndarray
+    states: Optional[np.ndarray] = None   # rho (n,4,9,9) or kets (n,4,9) (complex)
+    kernel_ms: float = 0.0
+
+    @property
+    def n(self):
+        return self.batch.n
+
+    def __len__(self):
+        return self.n
+
+    def point(self, i: int) -> Dict[str, Any]:
+        return dict(avg_fidelity=float(self.avg_fidelity[i]),
+                    fidelities=dict(zip(LABELS, map(float, self.fidelities[i]))),
+                    controlled_phase=float(self.controlled_phase[i]),
+                    cz_phase_fidelity=float(self.cz_phase_fidelity[i]),
+                    status=int(self.status[i]))
+
+
+_ENGINES: Dict[Tuple[int, ...], Any] = {}
+
+
+def _engine(devices=None):
+    from .engine import Engine
+    key = tuple(devices) if devices is not None else (0,)
+    if key not in _ENGINES:
+        _ENGINES[key] = Engine(list(key))
+    return _ENGINES[key]
+
+
+def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
+                           n_rydberg=70, qubit_0=(1, 0), qubit_1=(2, 0), hilbert_space_dim: int = 3,
+                           tweezer_power=30e-3, tweezer_waist=1.0e-6, tweezer_wavelength_nm=None,
+                           temperature=2e-6, B_field=1e-4, NA=0.5, spacing_factor=2.8,
+                           include_noise: bool = True, background_loss_rate_hz=None,
+                           trap_laser_on: bool = True, overrides: Optional[Dict[str, Any]] = None,
+                           phase_penalty: str = "reference", eigh=None, return_states: bool = False,
+                           devices=None, method: str = "chebyshev") -> BatchResult:
+    """Evaluate many simulate_CZ_gate points in one GPU pass (see module doc)."""
+    if hilbert_space_dim != 3:
+        if hilbert_space_dim == 4:
+            raise NotImplementedError("hilbert_space_dim=4 (mJ sublevels) is not yet on the GPU "
+                                      "engine (SURVEY.md §8f item 4)")
+        raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
+    from . import engine as E
+    b = PH.derive_batch(simulation_inputs, n, species=species, n_rydberg=n_rydberg, qubit_0=qubit_0,
+                        qubit_1=qubit_1, hilbert_space_dim=hilbert_space_dim,
+                        tweezer_power=tweezer_power, tweezer_waist=tweezer_waist,
+                        tweezer_wavelength_nm=tweezer_wavelength_nm, temperature=temperature,
+                        B_field=B_field, NA=NA, spacing_factor=spacing_factor,
+                        include_noise=include_noise, background_loss_rate_hz=background_loss_rate_hz,
+                        trap_laser_on=trap_laser_on, overrides=overrides)
+    key = E.protocol_key(b)
+    shape = b.pulse_shape.lower() if key == "lp_shaped" else "square"
+    nn = b.n
+    g = b.channel_rates()
+    # mesolve with an empty c_op list evolves kets (RG/simulation.py:683-690)
+    ket_mask = np.all([x == 0 for x in g], axis=0) if include_noise else np.ones(nn, bool)
+    fids = np.zeros((nn, 4))
+    pops = np.zeros((nn, 4))
+    cp = np.full(nn, np.nan)
+    pen = np.ones(nn)
+    status = np.zeros(nn, np.uint32)
+    states = None
+    if return_states:
+        states = {"ket": np.zeros((nn, 4, 9), complex), "rho": np.zeros((nn, 4, 9, 9), complex)}
+    eng = _engine(devices)
+    kms = 0.0
+    for evol, mask in (("ket", ket_mask), ("lindblad", ~ket_mask)):
+        idx = np.nonzero(mask)[0]
+        if idx.size == 0:
+            continue
+        r = eng.run(E.pack_params(b, idx), key, evol, shape=shape, method=method)
+        kms += r.kernel_ms
+        status[idx] = r.status
+        P = r.populations()
+        pops[idx] = P
+        if evol == "ket":
+            cp[idx] = r.col("CTRL_PHASE")
+            pen[idx] = r.col("PENALTY")
+            if return_states:
+                states["ket"][idx] = r.kets()
+        else:
+            need_rho = return_states or phase_penalty == "reference"
+            if need_rho:
+                for s0 in range(0, idx.size, 65536):
+                    sl = slice(s0, s0 + 65536)
+                    rho = E.expand_rho(r.state[:, 4 * s0:4 * (s0 + 65536)], min(65536, idx.size - s0))
+                    if phase_penalty == "reference":
+                        c_, p_ = mixed_phase_penalty(rho, eigh)
+                        cp[idx[sl]], pen[idx[sl]] = c_, p_
+                    if return_states:
+                        states["rho"][idx[sl]] = rho
+    fids[:] = pops
+    fids[:, 3] = pops[:, 3] * pen
+    avg = fids.mean(axis=1)
+    out_states = None
+    if return_states:
+        out_states = states
+    return BatchResult(batch=b, avg_fidelity=avg, fidelities=fids, populations=pops,
+                       controlled_phase=cp, cz_phase_fidelity=pen, status=status,
+                       is_mixed=~ket_mask, states=out_states, kernel_ms=kms)
+
+
+def _protocol_name(protocol: str) -> str:
+    return {"levine_pichler": "levine_pichler", "smooth_jp": "smooth_jp",
+            "jandura_pupillo": "jandura_pupillo"}[protocol]
+
+
+def simulate_CZ_gate(
+    simulation_inputs: Union[LPSimulationInputs, JPSimulationInputs, SmoothJPSimulationInputs],
+    config: AtomicConfiguration = None, species: str = "Rb87", n_rydberg: int = 70,
+    qubit_0: Tuple[int, int] = (1, 0), qubit_1: Tuple[int, int] = (2, 0),
+    hilbert_space_dim: int = 3, tweezer_power: float = 30e-3, tweezer_waist: float = 1.0e-6,
+    tweezer_wavelength_nm: float = None, temperature: float = 2e-6, B_field: float = 1e-4,
+    NA: float = 0.5, spacing_factor: float = 2.8, include_noise: bool = True,
+    background_loss_rate_hz: float = None, trap_laser_on: bool = True, verbose: bool = False,
+    return_dataclass: bool = True, *, eigh=None,
+) -> Union[SimulationResult, Dict]:
+    """Drop-in for RG/simulation.py:2534 (same arguments, same outputs) on the GPU engine."""
+    if config is None:
+        config = AtomicConfiguration(species=species, qubit_0=qubit_0, qubit_1=qubit_1,
+                                     n_rydberg=n_rydberg, L_rydberg="S")
+    br = simulate_CZ_gate_batch(
+        simulation_inputs, 1, species=config.species, n_rydberg=config.n_rydberg,
+        qubit_0=config.qubit_0, qubit_1=config.qubit_1, hilbert_space_dim=hilbert_space_dim,
+        tweezer_power=tweezer_power, tweezer_waist=tweezer_waist,
+        tweezer_wavelength_nm=tweezer_wavelength_nm, temperature=temperature, B_field=B_field,
+        NA=NA, spacing_factor=spacing_factor, include_noise=include_noise,
+        background_loss_rate_hz=background_loss_rate_hz, trap_laser_on=trap_laser_on,
+        phase_penalty="reference", eigh=eigh, return_states=True)
+    if br.status[0] != 0:
+        raise RuntimeError(f"GPU engine failed for this point (status bits {int(br.status[0])})")
+    b = br.batch
+    c = {k: (v[0] if np.ndim(v) > 0 else v) for k, v in b.cols.items()}
+    mixed = bool(br.is_mixed[0])
+    st = br.states["rho" if mixed else "ket"][0]
+    results = {lab: st[k] for k, lab in enumerate(LABELS)}
+    fidelities, avg, phase_info = compute_CZ_fidelity(results, True, hilbert_space_dim, eigh=eigh)
+    protocol = b.protocol
+    is_lp = protocol == "levine_pichler"
+    d1 = c["delta_zeeman"] + (c["delta_stark"] if trap_laser_on else 0.0)
+    H1 = H2 = None
+    xi = 1.0
+    if is_lp:
+        xi = complex(c["xi_re"], c["xi_im"])
+        H1 = OPS.hamiltonian(c["Omega"], c["Delta_gate"], c["V"], 3, d1)
+        H2 = OPS.hamiltonian(c["Omega"] * xi, c["Delta_gate"], c["V"], 3, d1)
+    rates = {k: c[k] for k in PH.RATE_FIELDS}
+    c_ops = OPS.collapse_operators(rates, hilbert_space_dim) if include_noise else []
+    si = simulation_inputs
+    noise_breakdown = {
+        "total_decay_rate": 0.0, "total_dephasing_rate": 0.0, "total_loss_rate": 0.0,
+        "n_collapse_ops": 0, "motional_dephasing_included": si.noise.include_motional_dephasing,
+        "gamma_scatter_intermediate": c["g_scatter"], "Omega1_MHz": c["Omega1"] / (2 * np.pi * 1e6),
+    }
+    if include_noise:
+        gphi = rates["gamma_phi_laser"] + rates["gamma_phi_thermal"] + rates["gamma_phi_zeeman"]
+        noise_breakdown.update(rates)
+        noise_breakdown.update(
+            branching_1=0.5, gamma_phi_total=gphi, total_decay_rate=rates["gamma_r"] + rates["gamma_bbr"],
+            total_dephasing_rate=gphi,
+            total_loss_rate=rates["gamma_loss_antitrap"] + rates["gamma_loss_background"] + rates["gamma_leakage"],
+            dim=hilbert_space_dim, n_collapse_ops=len(c_ops),
+            gamma_blockade_fluct=c["g_thermal"] if si.noise.include_motional_dephasing else 0.0,
+            gamma_doppler=c["g_doppler"], gamma_intensity_noise=c["g_intensity"],
+            gamma_thermal_total=rates["gamma_phi_thermal"],
+            delta_V_over_V_percent=c["dVV"] * 100, anti_trap_time_factor=c.get("anti_trap_time_factor", 0.0),
+            magic_enhancement=c["enhancement"], alpha_ratio=c["alpha_ratio"],
+            k_eff_rad_per_m=c["k_eff"], v_thermal_m_per_s=c["v_thermal"],
+            gamma_mJ_leakage=rates["mJ_leakage_rate"])
+    A0 = 0.529e-10
+    from .constants import EPS0
+    au = 4 * np.pi * EPS0 * A0 ** 3
+    magic = {"alpha_ratio": c["alpha_ratio"], "alpha_ground_au": c["alpha_g"] / au,
+             "alpha_rydberg_au": c["alpha_r"] / au, "gamma_antitrap_Hz": c["g_antitrap_raw"],
+             "differential_shift_Hz": c["diff_shift"], "magic_enhancement": c["enhancement"],
+             "wavelength_nm": c["wavelength_nm"]}
+    if protocol == "levine_pichler":
+        pulse_info = {"shape": b.pulse_shape, "implementation": "constant_hamiltonian"}
+        n_pulses = 2
+    elif protocol == "smooth_jp":
+        pulse_info = {"shape": "smooth_sinusoidal", "implementation": "time_dependent_hamiltonian",
+                      "protocol_variant": "bluvstein_evered_dark_state", "A": c["A"],
+                      "omega_mod_ratio": c["omega_mod"] / c["Omega"], "phi_offset": c["phi_offset"],
+                      "delta_over_omega": c["smooth_delta_over_omega"]}
+        n_pulses = 1
+    else:
+        pulse_info = {"shape": "bangbang", "implementation": "piecewise_constant_hamiltonian",
+                      "protocol_variant": "jandura_pupillo_bangbang",
+                      "switching_times": list(b.bangbang_times[0]), "phases": list(b.bangbang_phases[0]),
+                      "n_segments": b.bangbang_phases.shape[1], "omega_tau": c["omega_tau"]}
+        n_pulses = 1
+    pulse_info.update(delta_zeeman=c["delta_zeeman"], delta_stark=c["delta_stark"] if trap_laser_on else 0.0,
+                      trap_laser_on=trap_laser_on)
+    hs = SimpleNamespace(dim=hilbert_space_dim, basis=OPS.basis_kets(hilbert_space_dim))
+    rd = dict(
+        avg_fidelity=avg, fidelities=fidelities, phase_info=phase_info,
+        protocol=_protocol_name(protocol), n_pulses=n_pulses, hilbert_space_dim=hilbert_space_dim,
+        Omega=c["Omega"], V=c["V"], Delta=c["Delta_gate"], V_over_Omega=c["V_over_Omega"],
+        Delta_over_Omega=c["delta_over_omega"], tau_single=c["tau_single"], tau_total=c["tau_total"],
+        xi=xi, R=c["R"], spacing_factor=spacing_factor, U0_mK=c["U0"] / KB * 1e3,
+        omega_r_kHz=c["omega_r"] / (2 * np.pi * 1e3), sigma_r_nm=c["sigma_r"] * 1e9,
+        trap_wavelength_nm=c["wavelength_nm"], magic_wavelength_analysis=magic,
+        noise_breakdown=noise_breakdown, include_noise=include_noise,
+        include_motional_dephasing=si.noise.include_motional_dephasing, pulse_info=pulse_info,
+        config=config, species=config.species, n_rydberg=config.n_rydberg, qubit_0=config.qubit_0,
+        qubit_1=config.qubit_1, temperature_K=temperature, B_field_T=B_field,
+        delta_zeeman=c["delta_zeeman"], delta_stark=c["delta_stark"] if trap_laser_on else 0.0,
+        trap_laser_on=trap_laser_on, results=results, H1=H1, H2=H2, c_ops=c_ops, hs=hs)
+    if verbose:
+        print(f"  V/Ω = {rd['V_over_Omega']:.1f}; τ_total = {rd['tau_total'] * 1e6:.3f} µs; "
+              f"avg F = {avg:.6f}")
+    if return_dataclass:
+        return SimulationResult(**rd)
+    rd.update(Omega_rad_per_s=rd["Omega"], Omega_MHz=rd["Omega"] / (2 * np.pi * 1e6),
+              V_rad_per_s=rd["V"], V_MHz=rd["V"] / (2 * np.pi * 1e6), Delta_rad_per_s=rd["Delta"],
+              Delta_MHz=rd["Delta"] / (2 * np.pi * 1e6),
+              xi_rad=float(np.angle(xi)) if n_pulses == 2 else 0.0,
+              xi_deg=float(np.degrees(np.angle(xi))) if n_pulses == 2 else 0.0,
+              tau_single_us=rd["tau_single"] * 1e6, tau_total_us=rd["tau_total"] * 1e6,
+              gate_time_us=rd["tau_total"] * 1e6, R_meters=rd["R"], R_um=rd["R"] * 1e6,
+              temperature_uK=temperature * 1e6, B_field_Gauss=B_field * 1e4)
+    return rd

@@ -223,3 +223,25 @@ def test_edge_cases(eng):
     assert e0.state.shape == (25, 0)
     one = eng.run(p[:, :1], "lp_square", "ket")
     assert one.status[0] == 0 and abs(np.linalg.norm(one.kets()[0, 3]) - 1) < 1e-12
+
+
+@pytest.mark.parametrize("protocol,n_steps", [("lp_square", None), ("bangbang", None),
+                                              ("smooth_jp", 30)])
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_squaring_and_vector_methods_agree(eng, protocol, n_steps, symmetric):
+    """The propagator-squaring kernel and the per-input vector kernel are two
+    independent evaluations of the same exact propagator."""
+    rng = np.random.default_rng(11)
+    p = _random_points(rng, 45, protocol)           # 45 = 4.5 blocks of 10 points: ragged tail
+    if symmetric:
+        for k in ("G1", "G0", "GPHI", "GSC"):
+            p[N.P[k + "_B"]] = p[N.P[k + "_A"]]
+    rv = eng.run(p, protocol, "lindblad", n_steps=n_steps, method="cheb_vector")
+    rs = eng.run(p, protocol, "lindblad", n_steps=n_steps, method="cheb_squaring")
+    assert np.all(rv.status == 0) and np.all(rs.status == 0)
+    np.testing.assert_allclose(rs.state, rv.state, atol=1e-11, rtol=0)
+    np.testing.assert_allclose(rs.populations(), rv.populations(), atol=1e-12, rtol=0)
+    assert np.all(rs.col("NSQUARE") > 0) and np.all(rv.col("NSQUARE") == 0)
+    ref = _oracle_point(p, 44, protocol, n_steps=n_steps or 300)
+    for k, lab in enumerate(O.LABELS):
+        np.testing.assert_allclose(rs.rho()[44, k], ref[lab], atol=TOL, rtol=0)
