@@ -85,9 +85,7 @@ def main():
     from noisyquantumsimulator_amd import sweeps as SW
 
     # this rank's contiguous shard of the global N x 10k sweep (Delta/Omega partitioned)
-    n_delta_global = N_DELTA * ws
-    batch = SW.omega_delta_grid(N_OMEGA, n_delta_global, include_noise=True,
-                                delta_slice=slice(rank * N_DELTA, (rank + 1) * N_DELTA))
+    batch = SW.c2_rank_shard(rank, ws, N_DELTA, N_OMEGA)
     params = E.pack_params(batch)
     n = batch.n
     eng = E.Engine(devices=[local])

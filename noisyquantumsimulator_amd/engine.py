@@ -190,14 +190,16 @@ class Engine:
             pass
 
     def run(self, params: np.ndarray, protocol: str, evolution: str, n_steps: Optional[int] = None,
-            shape: str = "square", method: str = "chebyshev") -> EngineResult:
+            shape: str = "square", method: str = "chebyshev", rtol: float = 1e-10,
+            atol: float = 1e-12, max_steps: int = 10 ** 7) -> EngineResult:
         params = np.ascontiguousarray(params, dtype=np.float64)
         if params.shape[0] != N.NPARAM:
             raise ValueError(f"params must have shape ({N.NPARAM}, n)")
         n = params.shape[1]
         if n_steps is None:
             n_steps = default_n_steps(protocol, params)
-        desc = make_desc(protocol, evolution, n_steps, shape, symmetric_atoms(params), method)
+        desc = make_desc(protocol, evolution, n_steps, shape, symmetric_atoms(params), method,
+                         rtol=rtol, atol=atol, max_steps=max_steps)
         w = N.STATE_WIDTH[evolution]
         state = np.zeros((w, 4 * n), dtype=np.float64)
         summ = np.zeros((N.NSUMMARY, n), dtype=np.float64)

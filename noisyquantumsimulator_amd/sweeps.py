@@ -96,3 +96,15 @@ def species_temperature_power_grid(n_T: int = 1000, n_P: int = 500, include_nois
     return PH.derive_batch(CF.LPSimulationInputs(excitation=medium_excitation()), n=T_.size,
                            **_apparatus_kwargs(species=sp[S_], temperature=T_, tweezer_power=P_),
                            include_noise=include_noise)
+
+
+def c2_rank_shard(rank: int, world_size: int, points_per_rank_delta: int = 100,
+                  n_omega: int = 100, include_noise: bool = True) -> PH.DerivedBatch:
+    """Weak-scaling shard for multi-GPU runs: the global sweep has
+    world_size x 10k points (Delta/Omega grid refined world_size times) and rank r
+    owns the contiguous Delta/Omega range [r*100, (r+1)*100) -- no data exchange."""
+    if not 0 <= rank < world_size:
+        raise ValueError("rank out of range")
+    return omega_delta_grid(n_omega, points_per_rank_delta * world_size, include_noise=include_noise,
+                            delta_slice=slice(rank * points_per_rank_delta,
+                                              (rank + 1) * points_per_rank_delta))
