@@ -785,14 +785,17 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
 // Adaptive Dormand-Prince 5(4) kernel (RYD_METHOD_DOPRI5)
 // ---------------------------------------------------------------------------
 // The error-controlled stepper the north star names, fused in-kernel: one lane
-// per (point, basis input), the 25-coordinate state and the stages in VGPRs
-// (FSAL; y_new and the error are accumulated as soon as k6 exists so k1..k6
-// retire before k7), weighted-RMS error control as ZVODE/QuTiP
-// (atol + rtol*max|y|), exact stops at the reference's segment boundaries, a
-// step cap per segment (mesolve's nsteps, RG/simulation.py:687) -> status bit.
-// It needs ~15x the generator applications of the Chebyshev propagator at
-// 1e-10 accuracy (V*dt ~ 1e3 rad per pulse); it is kept as an independent
-// cross-check and as the reference-style comparison point.
+// per (point, basis input).  The state y, the stage input, the RHS output and the
+// error accumulator live in VGPRs; the stage derivatives k1..k6 are staged in LDS
+// (one private column per lane, [stage][coord][lane] so a wave's accesses are
+// conflict-free, no barriers needed).  FSAL, weighted-RMS error control as
+// ZVODE/QuTiP (atol + rtol*max|y|), exact stops at the reference's segment
+// boundaries, a step cap per segment (mesolve's nsteps, RG/simulation.py:687)
+// -> status bit.  It needs ~15x the generator applications of the Chebyshev
+// propagator at 1e-10 accuracy (V*dt ~ 1e3 rad per pulse); it is kept as an
+// independent cross-check and as the reference-style comparison point.
+constexpr int DP_BLOCK = 64;
+
 __device__ __forceinline__ void lindblad_rhs(const Gen& A, const Gen& B, double vs,
                                              const double (&y)[25], double (&f)[25]) {
 #pragma unroll
@@ -802,26 +805,44 @@ __device__ __forceinline__ void lindblad_rhs(const Gen& A, const Gen& B, double 
   apply_V(vs, y, f);
 }
 
+// Dormand & Prince (1980) tableau
+struct DP {
+  static constexpr double a[6][5] = {
+      {0, 0, 0, 0, 0},
+      {1.0 / 5, 0, 0, 0, 0},
+      {3.0 / 40, 9.0 / 40, 0, 0, 0},
+      {44.0 / 45, -56.0 / 15, 32.0 / 9, 0, 0},
+      {19372.0 / 6561, -25360.0 / 2187, 64448.0 / 6561, -212.0 / 729, 0},
+      {9017.0 / 3168, -355.0 / 33, 46732.0 / 5247, 49.0 / 176, -5103.0 / 18656}};
+  static constexpr double b[6] = {35.0 / 384, 0, 500.0 / 1113, 125.0 / 192, -2187.0 / 6784, 11.0 / 84};
+  static constexpr double e[6] = {71.0 / 57600, 0, -71.0 / 16695, 71.0 / 1920, -17253.0 / 339200,
+                                  22.0 / 525};
+  static constexpr double e7 = -1.0 / 40;
+};
+
+using KStore = double[6][25][DP_BLOCK];
+
+// tmp = y + hh * sum_{l<J} a[J][l] k_l   (k_l from this lane's LDS column)
+template <int J>
+__device__ __forceinline__ void dp_stage_input(const double (&y)[25], double hh, const KStore& ks, int lt,
+                                               double (&tmp)[25]) {
+#pragma unroll
+  for (int e = 0; e < 25; ++e) {
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < J; ++l) acc = fma(DP::a[J][l], ks[l][e][lt], acc);
+    tmp[e] = fma(hh, acc, y[e]);
+  }
+}
+
 template <int PROTO>
-__global__ __launch_bounds__(BLOCK) void lindblad_dopri5_kernel(
+__global__ __launch_bounds__(DP_BLOCK) void lindblad_dopri5_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ st, int64_t lds,
     double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape,
     double rtol, double atol, int64_t max_steps) {
-  // Dormand & Prince (1980) tableau
-  constexpr double c2 = 1.0 / 5, c3 = 3.0 / 10, c4 = 4.0 / 5, c5 = 8.0 / 9;
-  constexpr double a21 = 1.0 / 5;
-  constexpr double a31 = 3.0 / 40, a32 = 9.0 / 40;
-  constexpr double a41 = 44.0 / 45, a42 = -56.0 / 15, a43 = 32.0 / 9;
-  constexpr double a51 = 19372.0 / 6561, a52 = -25360.0 / 2187, a53 = 64448.0 / 6561, a54 = -212.0 / 729;
-  constexpr double a61 = 9017.0 / 3168, a62 = -355.0 / 33, a63 = 46732.0 / 5247, a64 = 49.0 / 176,
-                   a65 = -5103.0 / 18656;
-  constexpr double b1 = 35.0 / 384, b3 = 500.0 / 1113, b4 = 125.0 / 192, b5 = -2187.0 / 6784,
-                   b6 = 11.0 / 84;
-  constexpr double e1 = 71.0 / 57600, e3 = -71.0 / 16695, e4 = 71.0 / 1920, e5 = -17253.0 / 339200,
-                   e6 = 22.0 / 525, e7 = -1.0 / 40;
-  (void)c2; (void)c3; (void)c4; (void)c5;   // autonomous within a segment
-
-  const int64_t gid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  __shared__ KStore ks;                       // 6*25*64*8 = 75 KB
+  const int lt = threadIdx.x;
+  const int64_t gid = (int64_t)blockIdx.x * DP_BLOCK + lt;
   const bool live = gid < 4 * n;
   const int64_t i = live ? (gid >> 2) : (n - 1);
   const int inp = (int)(gid & 3);
@@ -839,6 +860,7 @@ __global__ __launch_bounds__(BLOCK) void lindblad_dopri5_kernel(
 #pragma unroll
   for (int c = 0; c < 4; ++c) rsum += fabs(q.gA[c]) + fabs(q.gB[c]);
   double h = 0.0;
+#pragma unroll 1
   for (int s = 0; s < nseg; ++s) {
     const Seg g = segment<PROTO>(q, s, n_steps, shape);
     double emin, emax;
@@ -848,49 +870,50 @@ __global__ __launch_bounds__(BLOCK) void lindblad_dopri5_kernel(
     const Gen A = make_gen(g, q.d1, q.gA, 1.0);
     const Gen B = make_gen(g, q.d1, q.gB, 1.0);
     const double vs = 0.5 * q.V;
-    double k1[25];
-    lindblad_rhs(A, B, vs, y, k1);           // fresh k1 at every segment start (new H)
+    double f[25], tmp[25];
+    lindblad_rhs(A, B, vs, y, f);             // fresh k1 at every segment start (new H)
+#pragma unroll
+    for (int e = 0; e < 25; ++e) ks[0][e][lt] = f[e];
     nrhs += 1.0;
     double t = 0.0;
-    if (h <= 0.0) h = 0.5 / omega;           // |h lambda| ~ 0.5 start
+    if (h <= 0.0) h = 0.5 / omega;            // |h lambda| ~ 0.5 start
     int64_t nst = 0;
     bool done = !active;
     while (__any(!done)) {
       if (!done) {
         const double hh = fmin(h, g.dt - t);
-        double k2[25], k3[25], k4[25], k5[25], tmp[25];
+        dp_stage_input<1>(y, hh, ks, lt, tmp);
+        lindblad_rhs(A, B, vs, tmp, f);
 #pragma unroll
-        for (int e = 0; e < 25; ++e) tmp[e] = fma(hh * a21, k1[e], y[e]);
-        lindblad_rhs(A, B, vs, tmp, k2);
+        for (int e = 0; e < 25; ++e) ks[1][e][lt] = f[e];
+        dp_stage_input<2>(y, hh, ks, lt, tmp);
+        lindblad_rhs(A, B, vs, tmp, f);
 #pragma unroll
-        for (int e = 0; e < 25; ++e) tmp[e] = y[e] + hh * (a31 * k1[e] + a32 * k2[e]);
-        lindblad_rhs(A, B, vs, tmp, k3);
+        for (int e = 0; e < 25; ++e) ks[2][e][lt] = f[e];
+        dp_stage_input<3>(y, hh, ks, lt, tmp);
+        lindblad_rhs(A, B, vs, tmp, f);
 #pragma unroll
-        for (int e = 0; e < 25; ++e) tmp[e] = y[e] + hh * (a41 * k1[e] + a42 * k2[e] + a43 * k3[e]);
-        lindblad_rhs(A, B, vs, tmp, k4);
+        for (int e = 0; e < 25; ++e) ks[3][e][lt] = f[e];
+        dp_stage_input<4>(y, hh, ks, lt, tmp);
+        lindblad_rhs(A, B, vs, tmp, f);
 #pragma unroll
-        for (int e = 0; e < 25; ++e)
-          tmp[e] = y[e] + hh * (a51 * k1[e] + a52 * k2[e] + a53 * k3[e] + a54 * k4[e]);
-        lindblad_rhs(A, B, vs, tmp, k5);
-#pragma unroll
-        for (int e = 0; e < 25; ++e)
-          tmp[e] = y[e] + hh * (a61 * k1[e] + a62 * k2[e] + a63 * k3[e] + a64 * k4[e] + a65 * k5[e]);
-        double k6[25];
-        lindblad_rhs(A, B, vs, tmp, k6);
-        double yn[25], er[25];
+        for (int e = 0; e < 25; ++e) ks[4][e][lt] = f[e];
+        dp_stage_input<5>(y, hh, ks, lt, tmp);
+        lindblad_rhs(A, B, vs, tmp, f);      // f = k6
 #pragma unroll
         for (int e = 0; e < 25; ++e) {
-          yn[e] = y[e] + hh * (b1 * k1[e] + b3 * k3[e] + b4 * k4[e] + b5 * k5[e] + b6 * k6[e]);
-          er[e] = hh * (e1 * k1[e] + e3 * k3[e] + e4 * k4[e] + e5 * k5[e] + e6 * k6[e]);
+          ks[5][e][lt] = f[e];
+          tmp[e] = y[e] + hh * (DP::b[0] * ks[0][e][lt] + DP::b[2] * ks[2][e][lt] + DP::b[3] * ks[3][e][lt] +
+                                DP::b[4] * ks[4][e][lt] + DP::b[5] * f[e]);
         }
-        double k7[25];
-        lindblad_rhs(A, B, vs, yn, k7);
+        lindblad_rhs(A, B, vs, tmp, f);      // f = k7 = f(y_new)
         nrhs += 6.0;
         double acc = 0.0;
 #pragma unroll
         for (int e = 0; e < 25; ++e) {
-          const double ee = fma(hh * e7, k7[e], er[e]);
-          const double sc = atol + rtol * fmax(fabs(y[e]), fabs(yn[e]));
+          const double ee = hh * (DP::e[0] * ks[0][e][lt] + DP::e[2] * ks[2][e][lt] + DP::e[3] * ks[3][e][lt] +
+                                  DP::e[4] * ks[4][e][lt] + DP::e[5] * ks[5][e][lt] + DP::e7 * f[e]);
+          const double sc = atol + rtol * fmax(fabs(y[e]), fabs(tmp[e]));
           const double r = ee / sc;
           acc = fma(r, r, acc);
         }
@@ -899,11 +922,12 @@ __global__ __launch_bounds__(BLOCK) void lindblad_dopri5_kernel(
         if (ok) {
 #pragma unroll
           for (int e = 0; e < 25; ++e) {
-            y[e] = yn[e];
-            k1[e] = k7[e];                    // FSAL
+            y[e] = tmp[e];
+            ks[0][e][lt] = f[e];               // FSAL
           }
+          const double rem = g.dt - t;
           t += hh;
-          if (hh >= g.dt - t + hh) done = true;   // reached the segment end exactly
+          if (hh >= rem) done = true;          // that was the step to the segment end
         }
         double fac = isfinite(err) ? 0.9 * pow(fmax(err, 1e-10), -0.2) : 0.2;
         fac = fmin(5.0, fmax(0.2, fac));
@@ -1061,14 +1085,14 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
       case RYD_PROTO_BANGBANG: f = lindblad_dopri5_kernel<RYD_PROTO_BANGBANG>; break;
       default: f = lindblad_dopri5_kernel<RYD_PROTO_SMOOTH_JP>; break;
     }
-    const int64_t blocks = (4 * n + BLOCK - 1) / BLOCK;
+    const int64_t blocks = (4 * n + DP_BLOCK - 1) / DP_BLOCK;
     int ns = d->n_steps, sh = d->shape;
     double rt = d->rtol, at = d->atol;
     int64_t ms = d->max_steps;
     void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
                     (void*)&ldm, (void*)&dstat, (void*)&ns, (void*)&sh, (void*)&rt, (void*)&at,
                     (void*)&ms};
-    HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(BLOCK), args, 0, stream));
+    HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(DP_BLOCK), args, 0, stream));
     return RYD_OK;
   }
   KernelFn k = pick_kernel(d);

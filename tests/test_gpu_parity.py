@@ -263,7 +263,7 @@ def test_multi_device_handle_range_partition():
 
 
 @pytest.mark.parametrize("protocol,n_steps", [("lp_square", None), ("bangbang", None),
-                                              ("smooth_jp", 20)])
+                                              ("smooth_jp", 3), ("smooth_jp", 20)])
 def test_dopri5_reference_stepper(eng, protocol, n_steps):
     """The adaptive RK45 (Dormand-Prince) mode agrees with the exact propagator to its
     tolerance; the step cap raises the STEP_CAP status bit instead of failing the batch."""
