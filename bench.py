@@ -1,10 +1,12 @@
 """Benchmark: Lindblad parameter points/s on the C2 sweep (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3]
 
 A step = one propagation of this rank's 10,000-point LP-square (Omega, Delta)
 sweep -- every point's 4 basis density matrices through both pulses, noise
-rates from the reference formulas -- with inputs resident in HBM.  With N > 1
+rates from the reference formulas -- with inputs resident in HBM.  ``--workload
+c3`` runs the 100k-point smooth-JP (Omega, Omega*tau) Pareto sweep instead
+(300 reference segments per point); it is a secondary line, not the metric.  With N > 1
 ranks (torch.distributed.run, one process per GPU) the global sweep is N x 10k
 points range-partitioned by Delta/Omega; no collective touches the data path
 (weak scaling); a gloo barrier brackets the timed region and the max time over
@@ -30,6 +32,22 @@ FLOP_PER_MATVEC = 2 * (75 + 75 + 12 + 25)
 FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
 FLOP_PER_STATE_UPDATE = 2 * 4 * 25 ** 2  # R_k <- U R_k for the 4 inputs, per segment
 N_OMEGA, N_DELTA = 100, 100
+# PMC-measured HBM bytes per launch of the dominant kernel (rocprofv3 --pmc FETCH_SIZE /
+# WRITE_SIZE in separate passes, FETCH_SIZE x2 per MI355X_MICROARCH.md), committed under
+# profiles/ by tools/pmc_traffic.py; matched on workload + method + points per launch.
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def _measured_traffic(workload: str, method: str, n: int):
+    try:
+        with open(TRAFFIC_FILE) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for r in rows:
+        if r.get("workload") == workload and r.get("method") == method and r.get("n") == n:
+            return r
+    return None
 
 
 def _dist():
@@ -78,18 +96,28 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--method", default="chebyshev",
                     choices=["chebyshev", "cheb_squaring", "cheb_vector"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3"])
     args = ap.parse_args()
 
     ws, rank, local, pg = _dist()
     from noisyquantumsimulator_amd import engine as E
     from noisyquantumsimulator_amd import sweeps as SW
 
-    # this rank's contiguous shard of the global N x 10k sweep (Delta/Omega partitioned)
-    batch = SW.c2_rank_shard(rank, ws, N_DELTA, N_OMEGA)
+    if args.workload == "c2":
+        # this rank's contiguous shard of the global N x 10k sweep (Delta/Omega partitioned)
+        batch = SW.c2_rank_shard(rank, ws, N_DELTA, N_OMEGA)
+        protocol, n_steps, n_seg = "lp_square", None, 2
+        workload = ("C2: 10k-point (Omega, Delta) LP-square CZ sweep per GPU, medium apparatus, "
+                    "full reference noise model (8 Lindblad channels)")
+    else:
+        batch = SW.c3_rank_shard(rank, ws)
+        protocol, n_steps, n_seg = "smooth_jp", 300, 300
+        workload = ("C3: 100k-point (Omega, Omega*tau) smooth-JP Pareto sweep per GPU, 300 "
+                    "reference segments, medium apparatus, full reference noise model")
     params = E.pack_params(batch)
     n = batch.n
     eng = E.Engine(devices=[local])
-    db = E.DeviceBatch(eng, params, "lp_square", "lindblad", method=args.method)
+    db = E.DeviceBatch(eng, params, protocol, "lindblad", n_steps=n_steps, method=args.method)
 
     for _ in range(args.warmup):
         db.launch()
@@ -114,10 +142,13 @@ def main():
     bytes_per_point = 8 * 15 + 8 * 100 + 8 * 19 + 4
     achieved_gbs = bytes_per_point * n / (k_ms * 1e-3) / 1e9
     nsq = float(res.col("NSQUARE").sum())
+    prop_kernel = args.method in ("cheb_squaring", "chebyshev")   # both workloads: auto -> prop
     flops = res.matvec_useful * FLOP_PER_MATVEC + nsq * FLOP_PER_SQUARING
-    if nsq > 0:
-        flops += 2 * n * FLOP_PER_STATE_UPDATE          # 2 segments per LP-square point
+    if prop_kernel:
+        flops += n_seg * n * FLOP_PER_STATE_UPDATE       # R <- U R once per reference segment
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
+    tr = _measured_traffic(args.workload, args.method, n)
+    traffic = tr["bytes_per_launch"] if tr else None
 
     total_points = n * ws * args.steps
     value = total_points / dt_max
@@ -127,20 +158,22 @@ def main():
         "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "C2: 10k-point (Omega, Delta) LP-square CZ sweep per GPU, "
-                               "medium apparatus, full reference noise model (8 Lindblad channels)",
-                   "points_per_gpu": n, "global_points": n * ws, "parallelism": f"range-shard x{ws}",
-                   "method": args.method + (" (auto: propagator squaring for LP square)"
+        "config": {"workload": workload, "points_per_gpu": n, "global_points": n * ws,
+                   "parallelism": f"range-shard x{ws}",
+                   "method": args.method + (" (auto: propagator kernel, phase frame)"
                                             if args.method == "chebyshev" else "")},
-        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
-                     "kernel_ms": k_ms, "bytes_per_launch": bytes_per_point * n},
-        "roofline_fp64": {"bound": "fp64_valu", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
-                          "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                          "flops_per_launch": flops,
-                          "exec_over_useful": res.matvec_exec / max(res.matvec_useful, 1)},
+        # The binding roof is FP64 arithmetic (MI355X dense FP64: 78.6 TF, the same for the
+        # matrix cores and the VALU; these kernels run on the FP64 VALU); the HBM view is
+        # kept beside it: the kernel moves ~1 kB per point against ~1 MFLOP.
+        "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
+                     "traffic": traffic, "kernel_ms": k_ms, "flops_per_launch": flops,
+                     "exec_over_useful": res.matvec_exec / max(res.matvec_useful, 1)},
+        "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_launch": bytes_per_point * n},
     }
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.workload == "c2":
         procs = max(1, min(16, os.cpu_count() or 1))
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, procs)
     if rank == 0:

@@ -66,12 +66,15 @@ extern "C" {
 #define RYD_EVOL_LINDBLAD 0     /* rho (c_ops present)                                   */
 #define RYD_EVOL_KET      1     /* Schrodinger (include_noise=False -> kets, :683-690)    */
 
-#define RYD_METHOD_CHEBYSHEV      0  /* auto: squaring for few long segments (LP square,
-                                         bang-bang, Lindblad), vector otherwise            */
+#define RYD_METHOD_CHEBYSHEV      0  /* auto (Lindblad): propagator kernel for LP square,
+                                         bang-bang and smooth JP, vector otherwise; kets:
+                                         vector                                            */
 #define RYD_METHOD_DOPRI5         1  /* adaptive Dormand-Prince 5(4) (reference-style stepper) */
 #define RYD_METHOD_CHEB_VECTOR    2  /* Chebyshev on the 4 input states, one lane each      */
 #define RYD_METHOD_CHEB_SQUARING  3  /* Chebyshev on 25 basis columns of exp(L dt/2^s),
-                                         then s squarings in LDS (Lindblad only)            */
+                                         then s squarings in LDS (Lindblad only); segments
+                                         that differ only in laser phase share one
+                                         propagator (LP square, smooth JP)                  */
 
 #define RYD_SHAPE_SQUARE   0
 #define RYD_SHAPE_GAUSSIAN 1

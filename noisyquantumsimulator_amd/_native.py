@@ -10,7 +10,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libryd_engine.so")
+# RYD_ENGINE_LIB selects an alternative build of the same library (tuning variants)
+LIB_PATH = os.environ.get("RYD_ENGINE_LIB") or os.path.join(_HERE, "libryd_engine.so")
 
 # keep in sync with include/ryd_engine.h
 RYD_ABI_VERSION = 1

@@ -603,21 +603,149 @@ __global__ __launch_bounds__(BLOCK) void ket_cheb_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Propagator-squaring kernel (few long constant segments: LP square, bang-bang)
+// Propagator-squaring kernel (LP square, bang-bang, smooth JP)
 // ---------------------------------------------------------------------------
-// Per segment and point: U = exp(L dt) on the 25-dim sector, built as
+// Per point, U = exp(L dt) on the 25-dim sector is built as
 //   (1) U0 = exp(L dt / 2^s): one basis column per lane (25 lanes per point),
 //       the same Chebyshev/Miller Clenshaw loop as above on x/2^s <= X_BASE;
 //   (2) s squarings U <- U U in LDS; each lane owns a 5x5 output tile
 //       (point p, row block rb, col block cb), 625 FMAs and ~200 LDS reads per
 //       squaring;
-//   (3) R_k <- U R_k for the 4 basis-input states (kept in LDS).
-// Work per segment is O(log x) instead of O(x): the x = 5000 segments of the
-// Omega/2pi = 1 MHz points cost ~12x less, and every point costs about the same,
-// which removes the launch's critical-path imbalance.
+// and the 4 basis-input states (kept in LDS) are advanced by R_k <- U R_k.
+// Work per propagator is O(log x) instead of O(x) and about the same for every
+// point, which removes the launch's critical-path imbalance.
+//
+// Phase frame.  Segments that differ only in the laser phase share one
+// propagator: with D = exp(i phi (P_r (x) 1 + 1 (x) P_r)), H(Omega e^{i phi}) =
+// D H(Omega) D^dag, and every collapse operator of the model maps to a phase
+// multiple of itself, so L(Omega e^{i phi}) = Q L(Omega) Q^T where Q = Q1 (x) Q1
+// and Q1 rotates the (ex, ey) coordinates by phi (Q1 = [[c, s], [-s, c]]).
+// Hence exp(L(Omega e^{i phi}) dt) = Q exp(L(Omega) dt) Q^T exactly:
+//   LP square  (RG/simulation.py:728-735): U_gate = Q(xi) U0 Q(xi)^T U0
+//   smooth JP  (RG/simulation.py:1698-1731): U_gate = prod_s Q_s U0 Q_s^T,
+// one propagator per point instead of 2 (LP) or n_steps (smooth JP).  The
+// state update between two matvecs is the rotation Q_{s+1}^T Q_s =
+// Q(phi_s - phi_{s+1}).  LP uses the frame only when |xi| = 1 to 1e-14 for the
+// whole block (xi from compute_phase_shift_xi always is; an ABI caller may pass
+// any xi), otherwise it builds both propagators.
 constexpr int PPB = 10;                     // points per 256-lane block (250 lanes used)
 constexpr int NC = 25;
-constexpr double X_BASE = 6.0;              // Chebyshev argument after scaling
+#ifndef RYD_X_BASE
+#define RYD_X_BASE 6.0
+#endif
+constexpr double X_BASE = RYD_X_BASE;       // Chebyshev argument after scaling
+
+template <int PROTO>
+constexpr bool phase_frame_protocol() {
+  return PROTO == RYD_PROTO_LP_SQUARE || PROTO == RYD_PROTO_SMOOTH_JP;
+}
+
+// (cos, sin) of the laser phase of segment s (the same arithmetic as segment<>)
+template <int PROTO>
+__device__ __forceinline__ void segment_phase(const PointP& q, int s, int n_steps, double& c, double& sn) {
+  if (PROTO == RYD_PROTO_LP_SQUARE) {
+    c = s == 0 ? 1.0 : q.xr;
+    sn = s == 0 ? 0.0 : q.xi;
+  } else {
+    const double dt = q.tau / (double)n_steps;
+    const double tm = (double)s * dt + dt / 2;
+    sincos(q.A * cos(q.wmod * tm - q.phoff), &sn, &c);
+  }
+}
+
+// Build U = exp(L(g) g.dt) for every point of the block into U[p] (block-uniform
+// control flow; lane (pl, j) computes column j, then its 5x5 tile in squarings).
+template <bool SYM>
+__device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& s_max, const PointP& q,
+                                                 const Seg& g, bool valid, bool lane_ok, int t, int pl,
+                                                 int j, double& nuse, double& nexec, double& nsq,
+                                                 bool& over_cap) {
+  const int rb = j / 5, cb = j % 5;
+  double rsum = 0.0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) rsum += fabs(q.gA[c]) + fabs(q.gB[c]);
+  double emin, emax;
+  h_bounds(g, q.V, q.d1, emin, emax);
+  const double omega = (emax - emin) + rsum;
+  const double x = omega * g.dt;
+  const bool capped = valid && !(x <= 1e12);
+  const bool active = valid && !capped && x > X_SKIP && lane_ok;
+  over_cap = over_cap || capped;
+  int sq = 0;
+  if (active && x > X_BASE) sq = (int)ceil(log2(x / X_BASE));
+  const double y = active ? ldexp(x, -sq) : 0.0;
+  const double sc = active ? 2.0 / omega : 0.0;
+  const Gen A = make_gen(g, q.d1, q.gA, sc);
+  const Gen B = make_gen(g, q.d1, q.gB, sc);
+  const double vs = sc * 0.5 * q.V;
+  // (1) column j of exp(y Y)
+  double v[25];
+#pragma unroll
+  for (int e = 0; e < 25; ++e) v[e] = (e == j) ? 1.0 : 0.0;
+  cheb_segment<25>(v, y, active,
+                   [&](const double (&b)[25], double (&o)[25]) { apply_L<SYM>(A, B, vs, b, o); },
+                   nuse, nexec);
+  if (t == 0) s_max = 0;
+  __syncthreads();
+  if (lane_ok) {
+#pragma unroll
+    for (int r = 0; r < 25; ++r) U[pl][r][j] = v[r];
+    atomicMax(&s_max, sq);
+  }
+  __syncthreads();
+  const int smx = s_max;
+  nsq += (double)sq;
+  // (2) squarings: tile (rb, cb) of U U
+  for (int it = 0; it < smx; ++it) {
+    double acc[5][5];
+#pragma unroll
+    for (int a = 0; a < 5; ++a)
+#pragma unroll
+      for (int b = 0; b < 5; ++b) acc[a][b] = 0.0;
+    if (lane_ok && it < sq) {
+#ifdef RYD_SQ_UNROLL
+#pragma unroll RYD_SQ_UNROLL
+#endif
+      for (int k = 0; k < NC; ++k) {
+        double ar[5], bc[5];
+#pragma unroll
+        for (int a = 0; a < 5; ++a) ar[a] = U[pl][5 * rb + a][k];
+#pragma unroll
+        for (int b = 0; b < 5; ++b) bc[b] = U[pl][k][5 * cb + b];
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+#pragma unroll
+          for (int b = 0; b < 5; ++b) acc[a][b] = fma(ar[a], bc[b], acc[a][b]);
+      }
+    }
+    __syncthreads();
+    if (lane_ok && it < sq) {
+#pragma unroll
+      for (int a = 0; a < 5; ++a)
+#pragma unroll
+        for (int b = 0; b < 5; ++b) U[pl][5 * rb + a][5 * cb + b] = acc[a][b];
+    }
+    __syncthreads();
+  }
+}
+
+// dst_k[j] = (Q(c,s) R_k)[j] for this lane's coordinate j = 5a + b, Q = Q1 (x) Q1:
+// coordinate 3 -> c r3 + s r4, coordinate 4 -> -s r3 + c r4 on each atom index.
+__device__ __forceinline__ void rotate_coord(const double (&src)[4][NC], double (&dst)[4][NC], int j,
+                                            double c, double s) {
+  const int a = j / 5, b = j % 5;
+  const int a0 = a < 3 ? a : 3, b0 = b < 3 ? b : 3;
+  // weights of (a0, a0+1) and (b0, b0+1); non-rotating indices use (1, 0)
+  const double wa0 = a < 3 ? 1.0 : (a == 3 ? c : -s), wa1 = a < 3 ? 0.0 : (a == 3 ? s : c);
+  const double wb0 = b < 3 ? 1.0 : (b == 3 ? c : -s), wb1 = b < 3 ? 0.0 : (b == 3 ? s : c);
+  const int a1 = a < 3 ? a0 : a0 + 1, b1 = b < 3 ? b0 : b0 + 1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const double r00 = src[k][5 * a0 + b0], r01 = src[k][5 * a0 + b1];
+    const double r10 = src[k][5 * a1 + b0], r11 = src[k][5 * a1 + b1];
+    dst[k][j] = wa0 * (wb0 * r00 + wb1 * r01) + wa1 * (wb0 * r10 + wb1 * r11);
+  }
+}
 
 template <int PROTO, bool SYM>
 __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
@@ -625,17 +753,23 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
     double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
   __shared__ __attribute__((aligned(16))) double U[PPB][NC][NC];    // row-major U[p][row][col]
   __shared__ __attribute__((aligned(16))) double Rs[PPB][4][NC];    // basis-input states
+  __shared__ __attribute__((aligned(16))) double Rt[PPB][4][NC];    // rotated states (frame path)
   __shared__ int s_max;
 
   const int t = threadIdx.x;
   const bool lane_ok = t < PPB * NC;
   const int pl = lane_ok ? t / NC : 0;     // point within block
-  const int j = t % NC;                    // column (phase 1) / tile id (phase 2)
+  const int j = t % NC;                    // column (phase 1) / tile id (phase 2) / coordinate
   const int64_t ip = (int64_t)blockIdx.x * PPB + pl;
   const bool live = lane_ok && ip < n;
   const int64_t i = ip < n ? ip : n - 1;
-  const bool valid = point_valid<PROTO>(load_point<PROTO>(prm, ldp, i), n_steps);
-  const int rb = j / 5, cb = j % 5;        // 5x5 tile of the point's 25x25 product
+  bool valid, frame_ok;
+  {
+    const PointP q0 = load_point<PROTO>(prm, ldp, i);
+    valid = point_valid<PROTO>(q0, n_steps);
+    frame_ok = !(PROTO == RYD_PROTO_LP_SQUARE) || !valid ||
+               fabs(q0.xr * q0.xr + q0.xi * q0.xi - 1.0) <= 1e-14;
+  }
 
   for (int e = t; e < PPB * 4 * NC; e += BLOCK) {
     const int p = e / (4 * NC), k = (e / NC) % 4, r = e % NC;
@@ -645,94 +779,77 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
   double nuse = 0.0, nexec = 0.0, nsq = 0.0;
   bool over_cap = false;
   const int nseg = n_segments<PROTO>(n_steps);
+  const bool use_frame = phase_frame_protocol<PROTO>() && __syncthreads_and(frame_ok || !lane_ok);
 
-  for (int s = 0; s < nseg; ++s) {
+  // one propagator per segment, or a single phase-0 propagator in the frame path
+  const int nprop = use_frame ? 1 : nseg;
+  for (int s = 0; s < nprop; ++s) {
     // re-read this point's scalars every segment (L1/L2 hits) instead of keeping
     // them live across the loop: the Chebyshev phase needs the VGPRs
     const double* pp = prm;
     asm volatile("" : "+s"(pp));
     const PointP q = load_point<PROTO>(pp, ldp, i);
-    double rsum = 0.0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) rsum += fabs(q.gA[c]) + fabs(q.gB[c]);
-    const Seg g = segment<PROTO>(q, s, n_steps, shape);
-    double emin, emax;
-    h_bounds(g, q.V, q.d1, emin, emax);
-    const double omega = (emax - emin) + rsum;
-    const double x = omega * g.dt;
-    const bool capped = valid && !(x <= 1e12);
-    const bool active = valid && !capped && x > X_SKIP && lane_ok;
-    over_cap = over_cap || capped;
-    int sq = 0;
-    if (active && x > X_BASE) sq = (int)ceil(log2(x / X_BASE));
-    const double y = active ? ldexp(x, -sq) : 0.0;
-    const double sc = active ? 2.0 / omega : 0.0;
-    const Gen A = make_gen(g, q.d1, q.gA, sc);
-    const Gen B = make_gen(g, q.d1, q.gB, sc);
-    const double vs = sc * 0.5 * q.V;
-    // (1) column j of exp(y Y)
-    double v[25];
-#pragma unroll
-    for (int e = 0; e < 25; ++e) v[e] = (e == j) ? 1.0 : 0.0;
-    cheb_segment<25>(v, y, active,
-                     [&](const double (&b)[25], double (&o)[25]) { apply_L<SYM>(A, B, vs, b, o); },
-                     nuse, nexec);
-    if (t == 0) s_max = 0;
-    __syncthreads();
-    if (lane_ok) {
-#pragma unroll
-      for (int r = 0; r < 25; ++r) {
-        U[pl][r][j] = v[r];
-      }
-      atomicMax(&s_max, sq);
+    Seg g = segment<PROTO>(q, s, n_steps, shape);
+    if (use_frame) {                         // reference frame: phase 0
+      g.om_re = q.Om;
+      g.om_im = 0.0;
     }
-    __syncthreads();
-    const int smx = s_max;
-    nsq += (double)sq;
-    // (2) squarings: tile (rb, cb) of U U
-    for (int it = 0; it < smx; ++it) {
-      double acc[5][5];
+    build_propagator<SYM>(U, s_max, q, g, valid, lane_ok, t, pl, j, nuse, nexec, nsq, over_cap);
+    if (!use_frame) {
+      // R_k <- U R_k ; lane (pl, r = j) computes row r for the 4 inputs
+      double nr[4] = {0.0, 0.0, 0.0, 0.0};
+      if (lane_ok) {
+        for (int m = 0; m < NC; ++m) {
+          const double u = U[pl][j][m];
 #pragma unroll
-      for (int a = 0; a < 5; ++a)
-#pragma unroll
-        for (int b = 0; b < 5; ++b) acc[a][b] = 0.0;
-      if (lane_ok && it < sq) {
-        for (int k = 0; k < NC; ++k) {
-          double ar[5], bc[5];
-#pragma unroll
-          for (int a = 0; a < 5; ++a) ar[a] = U[pl][5 * rb + a][k];
-#pragma unroll
-          for (int b = 0; b < 5; ++b) bc[b] = U[pl][k][5 * cb + b];    // U[k][5cb+b]
-#pragma unroll
-          for (int a = 0; a < 5; ++a)
-#pragma unroll
-            for (int b = 0; b < 5; ++b) acc[a][b] = fma(ar[a], bc[b], acc[a][b]);
+          for (int k = 0; k < 4; ++k) nr[k] = fma(u, Rs[pl][k][m], nr[k]);
         }
       }
       __syncthreads();
-      if (lane_ok && it < sq) {
+      if (lane_ok) {
 #pragma unroll
-        for (int a = 0; a < 5; ++a)
-#pragma unroll
-          for (int b = 0; b < 5; ++b) {
-            U[pl][5 * rb + a][5 * cb + b] = acc[a][b];
-          }
+        for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
       }
       __syncthreads();
     }
-    // (3) R_k <- U R_k ; lane (pl, r = j) computes row r for the 4 inputs
-    double nr[4] = {0.0, 0.0, 0.0, 0.0};
-    if (lane_ok) {
-      for (int m = 0; m < NC; ++m) {
-        const double u = U[pl][j][m];
+  }
+
+  if (use_frame) {
+    // U0 row j stays in registers for every segment
+    double u[NC];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) nr[k] = fma(u, Rs[pl][k][m], nr[k]);
+    for (int m = 0; m < NC; ++m) u[m] = U[pl][j][m];
+    double cp = 1.0, sp = 0.0;               // phase of the frame R is currently in
+    for (int s = 0; s < nseg; ++s) {
+      const double* pp = prm;
+      asm volatile("" : "+s"(pp));
+      const PointP q = load_point<PROTO>(pp, ldp, i);
+      double c, sn;
+      segment_phase<PROTO>(q, s, n_steps, c, sn);
+      // into this segment's frame: Q_s^T Q_{s-1} = Q(phi_{s-1} - phi_s)
+      const double cr = cp * c + sp * sn, sr = sp * c - cp * sn;
+      if (lane_ok) rotate_coord(Rs[pl], Rt[pl], j, cr, sr);
+      __syncthreads();
+      double nr[4] = {0.0, 0.0, 0.0, 0.0};
+      if (lane_ok) {
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) nr[k] = fma(u[m], Rt[pl][k][m], nr[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
       }
+      __syncthreads();
+      cp = c;
+      sp = sn;
     }
+    // back to the lab frame: Q_{N-1}
+    if (lane_ok) rotate_coord(Rs[pl], Rt[pl], j, cp, sp);
     __syncthreads();
     if (lane_ok) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
+      for (int k = 0; k < 4; ++k) Rs[pl][k][j] = Rt[pl][k][j];
     }
     __syncthreads();
   }
@@ -1008,12 +1125,21 @@ int fail(int code, const std::string& msg) {
 using KernelFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, double*, int64_t,
                           uint32_t*, int, int);
 
+// Lindblad runs on the propagator kernel when asked for explicitly, or under the
+// auto method for the protocols whose gate is a product of few propagators: LP
+// square and bang-bang (few long segments), smooth JP (one propagator in the
+// phase frame).  LP shaped (amplitude changes every segment) stays on the
+// state-vector Chebyshev kernel.
+bool use_propagator(const ryd_batch_desc* d) {
+  const bool auto_prop = d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG ||
+                         d->protocol == RYD_PROTO_SMOOTH_JP;
+  return d->evolution == RYD_EVOL_LINDBLAD &&
+         (d->method == RYD_METHOD_CHEB_SQUARING || (d->method == RYD_METHOD_CHEBYSHEV && auto_prop));
+}
+
 KernelFn pick_kernel(const ryd_batch_desc* d) {
   const bool sym = (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0;
-  const bool few_long = d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG;
-  const bool squaring = d->method == RYD_METHOD_CHEB_SQUARING ||
-                        (d->method == RYD_METHOD_CHEBYSHEV && few_long);
-  if (d->evolution == RYD_EVOL_LINDBLAD && squaring) {
+  if (use_propagator(d)) {
     if (d->protocol == RYD_PROTO_LP_SQUARE)
       return sym ? lindblad_prop_kernel<RYD_PROTO_LP_SQUARE, true> : lindblad_prop_kernel<RYD_PROTO_LP_SQUARE, false>;
     if (d->protocol == RYD_PROTO_BANGBANG)
@@ -1097,11 +1223,7 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
   }
   KernelFn k = pick_kernel(d);
   if (!k) return fail(RYD_ERR_UNSUPPORTED, "no kernel for this descriptor");
-  const bool few_long = d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG;
-  const bool squaring = d->evolution == RYD_EVOL_LINDBLAD &&
-                        (d->method == RYD_METHOD_CHEB_SQUARING ||
-                         (d->method == RYD_METHOD_CHEBYSHEV && few_long));
-  const int64_t blocks = squaring ? (n + PPB - 1) / PPB : (4 * n + BLOCK - 1) / BLOCK;
+  const int64_t blocks = use_propagator(d) ? (n + PPB - 1) / PPB : (4 * n + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
   int ns = d->n_steps, sh = d->shape;
   void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,

@@ -62,8 +62,8 @@ def omega_delta_grid(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.
                            overrides=dict(laser_2_power=p2, delta_over_omega=DOM.ravel()))
 
 
-def pareto_tgate_grid(n_omega: int = 1000, n_tau: int = 100, include_noise: bool = True
-                      ) -> PH.DerivedBatch:
+def pareto_tgate_grid(n_omega: int = 1000, n_tau: int = 100, include_noise: bool = True,
+                      omega_slice: Optional[slice] = None) -> PH.DerivedBatch:
     """C3: smooth-JP fidelity vs t_gate: Omega/2pi in linspace(1,10) MHz x Omega*tau in
     linspace(5, 25), medium apparatus (reference noise model)."""
     warnings.simplefilter("ignore")
@@ -72,6 +72,8 @@ def pareto_tgate_grid(n_omega: int = 1000, n_tau: int = 100, include_noise: bool
                           include_noise=False)
     om0 = ref["Omega"][0]
     om = 2 * np.pi * 1e6 * np.linspace(1, 10, n_omega)
+    if omega_slice is not None:
+        om = om[omega_slice]
     ot = np.linspace(5, 25, n_tau)
     OM, OT = np.meshgrid(om, ot, indexing="ij")
     p2 = MEDIUM["laser_2_power"] * (OM.ravel() / om0) ** 2
@@ -108,3 +110,13 @@ def c2_rank_shard(rank: int, world_size: int, points_per_rank_delta: int = 100,
     return omega_delta_grid(n_omega, points_per_rank_delta * world_size, include_noise=include_noise,
                             delta_slice=slice(rank * points_per_rank_delta,
                                               (rank + 1) * points_per_rank_delta))
+
+
+def c3_rank_shard(rank: int, world_size: int, n_omega_per_rank: int = 1000, n_tau: int = 100,
+                  include_noise: bool = True) -> PH.DerivedBatch:
+    """Weak-scaling shard of the C3 smooth-JP Pareto sweep: world_size x 100k points,
+    the Omega axis refined world_size times, rank r owning a contiguous Omega range."""
+    if not 0 <= rank < world_size:
+        raise ValueError("rank out of range")
+    return pareto_tgate_grid(n_omega_per_rank * world_size, n_tau, include_noise=include_noise,
+                             omega_slice=slice(rank * n_omega_per_rank, (rank + 1) * n_omega_per_rank))

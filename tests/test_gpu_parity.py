@@ -226,7 +226,7 @@ def test_edge_cases(eng):
 
 
 @pytest.mark.parametrize("protocol,n_steps", [("lp_square", None), ("bangbang", None),
-                                              ("smooth_jp", 30)])
+                                              ("smooth_jp", 30), ("smooth_jp", 300)])
 @pytest.mark.parametrize("symmetric", [True, False])
 def test_squaring_and_vector_methods_agree(eng, protocol, n_steps, symmetric):
     """The propagator-squaring kernel and the per-input vector kernel are two
@@ -247,6 +247,35 @@ def test_squaring_and_vector_methods_agree(eng, protocol, n_steps, symmetric):
     ref = _oracle_point(p, 44, protocol, n_steps=n_steps or 300)
     for k, lab in enumerate(O.LABELS):
         np.testing.assert_allclose(rs.rho()[44, k], ref[lab], atol=TOL, rtol=0)
+
+
+def test_lp_phase_frame_fallback_for_non_unit_xi(eng):
+    """LP square runs both pulses off ONE propagator (pulse 2 = pulse 1 in the frame
+    rotated by arg xi) when |xi| = 1, as compute_phase_shift_xi guarantees.  An ABI
+    caller may pass any xi: a block holding a non-unit xi builds both propagators
+    (NSQUARE doubles for its 10 points) and still matches the vector kernel."""
+    rng = np.random.default_rng(5)
+    p = _random_points(rng, 25, "lp_square")
+    base = eng.run(p, "lp_square", "lindblad", method="cheb_squaring")
+    q = p.copy()
+    q[N.P["XI_RE"], 13] *= 1.01
+    q[N.P["XI_IM"], 13] *= 1.01
+    rs = eng.run(q, "lp_square", "lindblad", method="cheb_squaring")
+    rv = eng.run(q, "lp_square", "lindblad", method="cheb_vector")
+    assert np.all(rs.status == 0)
+    np.testing.assert_allclose(rs.state, rv.state, atol=1e-11, rtol=0)
+    nb, nq = base.col("NSQUARE"), rs.col("NSQUARE")
+    blk = (np.arange(25) // 10 == 1) & (np.arange(25) != 13)   # 13's pulse 2 has a new x
+    np.testing.assert_array_equal(nq[blk], 2 * nb[blk])
+    out = np.arange(25) // 10 != 1
+    np.testing.assert_array_equal(nq[out], nb[out])
+    others = np.ones(25, bool)
+    others[13] = False
+    np.testing.assert_allclose(rs.state.reshape(25, 25, 4)[:, others],
+                               base.state.reshape(25, 25, 4)[:, others], atol=1e-12, rtol=0)
+    ref = _oracle_point(q, 13, "lp_square")
+    for k, lab in enumerate(O.LABELS):
+        np.testing.assert_allclose(rs.rho()[13, k], ref[lab], atol=TOL, rtol=0)
 
 
 def test_multi_device_handle_range_partition():
