@@ -30,6 +30,7 @@ FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (spec)
 # FLOPs per generator application (one 25-vector): apply_A 75 + apply_B 75 + V 12 + Clenshaw 25 FMAs
 FLOP_PER_MATVEC = 2 * (75 + 75 + 12 + 25)
 FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
+FLOP_PER_SQUARING_SYM = 2 * (15 ** 3 + 10 ** 3)   # identical atoms: sym (+) antisym blocks
 FLOP_PER_STATE_UPDATE = 2 * 4 * 25 ** 2  # R_k <- U R_k for the 4 inputs, per segment
 N_OMEGA, N_DELTA = 100, 100
 # PMC-measured HBM bytes per launch of the dominant kernel (rocprofv3 --pmc FETCH_SIZE /
@@ -143,7 +144,8 @@ def main():
     achieved_gbs = bytes_per_point * n / (k_ms * 1e-3) / 1e9
     nsq = float(res.col("NSQUARE").sum())
     prop_kernel = args.method in ("cheb_squaring", "chebyshev")   # both workloads: auto -> prop
-    flops = res.matvec_useful * FLOP_PER_MATVEC + nsq * FLOP_PER_SQUARING
+    sq_flops = FLOP_PER_SQUARING_SYM if E.symmetric_atoms(params) else FLOP_PER_SQUARING
+    flops = res.matvec_useful * FLOP_PER_MATVEC + nsq * sq_flops
     if prop_kernel:
         flops += n_seg * n * FLOP_PER_STATE_UPDATE       # R <- U R once per reference segment
     achieved_tf = flops / (k_ms * 1e-3) / 1e12

@@ -124,6 +124,26 @@ extern "C" {
 #define RYD_S_NSQUARE    19  /* 25x25 squarings performed (squaring method)               */
 #define RYD_NSUMMARY     20
 
+/* ---- process-map coherences (ryd_run_coherences), rows of out_coh ----------
+ * The qubit process map of the gate (the reference's
+ * top-level noise_models/ Kraus/CPTP extraction, src/qpu_simulator/noise_models/
+ * __init__.py:1-22, is a stub): the diagonal inputs |x><x| come from
+ * ryd_run_batch (Lindblad state rows); the 6 upper off-diagonal qubit matrix
+ * units |a><b| are evolved here, each in its excitation-number sector, and their
+ * images projected on the qubit block are returned as (re, im) row pairs:
+ *   RYD_C_K0 + 4s + 2o    input s in {|00><01|, |10><11|}, output coefficient
+ *                         o in {|00><01|, |10><11|}
+ *   RYD_C_K1 + 4s + 2o    input s in {|00><10|, |01><11|}, output o in {|00><10|, |01><11|}
+ *   RYD_C_K2              |00><11| -> coefficient of |00><11|
+ *   RYD_C_K3              |01><10| -> coefficient of |01><10|
+ * (no other qubit-block element is reachable from these inputs; the remaining
+ * 6 units are the adjoints).                                                   */
+#define RYD_C_K0   0
+#define RYD_C_K1   8
+#define RYD_C_K2  16
+#define RYD_C_K3  18
+#define RYD_NCOH  20
+
 /* ---- per-point status bits ---- */
 #define RYD_STATUS_NONFINITE   1u
 #define RYD_STATUS_STEP_CAP    2u   /* DOPRI5 step cap (ZVODE nsteps analogue)          */
@@ -183,6 +203,18 @@ int ryd_run_batch_device(ryd_handle* h, int slot, const ryd_batch_desc* desc,
                          double* d_state, int64_t ld_state,
                          double* d_summary, int64_t ld_summary,
                          uint32_t* d_status, void* stream, float* elapsed_ms);
+
+/* Process-map coherences (layout above).  Chebyshev state-vector method; any
+ * protocol, either evolution value (rates may be zero).  Host-buffer form
+ * range-partitions like ryd_run_batch; status bits as ryd_run_batch. */
+int ryd_run_coherences(ryd_handle* h, const ryd_batch_desc* desc,
+                       const double* params, int64_t n, int64_t ld_params,
+                       double* out_coh, int64_t ld_coh,
+                       uint32_t* out_status, ryd_stats* stats);
+int ryd_run_coherences_device(ryd_handle* h, int slot, const ryd_batch_desc* desc,
+                              const double* d_params, int64_t n, int64_t ld_params,
+                              double* d_coh, int64_t ld_coh, uint32_t* d_status,
+                              void* stream, float* elapsed_ms);
 
 /* Minimal device-memory plumbing so callers need no other GPU runtime. */
 int ryd_malloc(ryd_handle* h, int slot, size_t bytes, void** d_ptr);

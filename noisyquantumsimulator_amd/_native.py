@@ -31,11 +31,14 @@ S = dict(POP0=0, OV_RE0=4, OV_IM0=8, AVG_POP=12, CTRL_PHASE=13, PENALTY=14, AVG_
 NSUMMARY = 20
 STATUS_NONFINITE, STATUS_STEP_CAP, STATUS_BAD_INPUT = 1, 2, 4
 STATE_WIDTH = {"lindblad": 25, "ket": 18}
+# process-map coherence rows (ryd_run_coherences)
+C = dict(K0=0, K1=8, K2=16, K3=18)
+NCOH = 20
 
 EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary_width",
             "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",
-            "ryd_run_batch_device", "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h",
-            "ryd_synchronize")
+            "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
+            "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize")
 
 
 class BatchDesc(ctypes.Structure):
@@ -85,6 +88,10 @@ def load() -> ctypes.CDLL:
                                       ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(Stats)]
         lib.ryd_run_batch_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(BatchDesc), vp, i64, i64,
                                              vp, i64, vp, i64, vp, vp, ctypes.POINTER(ctypes.c_float)]
+        lib.ryd_run_coherences.argtypes = [vp, ctypes.POINTER(BatchDesc), dp, i64, i64, dp, i64,
+                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(Stats)]
+        lib.ryd_run_coherences_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(BatchDesc), vp, i64,
+                                                  i64, vp, i64, vp, vp, ctypes.POINTER(ctypes.c_float)]
         lib.ryd_malloc.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]
         lib.ryd_free.argtypes = [vp, ctypes.c_int, vp]
         lib.ryd_memcpy_h2d.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]

@@ -35,6 +35,12 @@
 
 #include "../../include/ryd_engine.h"
 
+// one stream per device slot; defined at global scope (the header's opaque type)
+struct ryd_handle {
+  std::vector<int> dev;
+  std::vector<hipStream_t> stream;
+};
+
 namespace {
 
 constexpr int BLOCK = 256;
@@ -630,10 +636,14 @@ __global__ __launch_bounds__(BLOCK) void ket_cheb_kernel(
 // any xi), otherwise it builds both propagators.
 constexpr int PPB = 10;                     // points per 256-lane block (250 lanes used)
 constexpr int NC = 25;
-#ifndef RYD_X_BASE
-#define RYD_X_BASE 6.0
+// Chebyshev argument after scaling.  Lower means fewer Chebyshev terms and more
+// squarings: with the cheap exchange-symmetric squaring (4375 FMAs) 2 is best, with
+// the full 25^3 one 3-6 are equal (profiles/r01/tune_*).  RYD_X_BASE overrides both.
+#ifdef RYD_X_BASE
+constexpr double X_BASE_SYM = RYD_X_BASE, X_BASE_FULL = RYD_X_BASE;
+#else
+constexpr double X_BASE_SYM = 2.0, X_BASE_FULL = 6.0;
 #endif
-constexpr double X_BASE = RYD_X_BASE;       // Chebyshev argument after scaling
 
 template <int PROTO>
 constexpr bool phase_frame_protocol() {
@@ -653,14 +663,29 @@ __device__ __forceinline__ void segment_phase(const PointP& q, int s, int n_step
   }
 }
 
-// Build U = exp(L(g) g.dt) for every point of the block into U[p] (block-uniform
-// control flow; lane (pl, j) computes column j, then its 5x5 tile in squarings).
+// Exchange symmetry (identical atoms, SYM): L commutes with the atom swap R -> R^T,
+// so in the orthonormal basis {sym_s = (E_ij + E_ji)/sqrt2 (i<j), E_ii ; asym_a =
+// (E_ij - E_ji)/sqrt2 (i<j)} the propagator is block-diagonal, U = Us (15x15) (+)
+// Ua (10x10).  A squaring then costs 15^3 + 10^3 = 4375 FMAs instead of 25^3.
+__host__ __device__ constexpr int sym_index(int i, int j) {      // i <= j
+  return i * 5 - i * (i - 1) / 2 + (j - i);
+}
+__host__ __device__ constexpr int asym_index(int i, int j) {     // i < j
+  return i * 4 - i * (i - 1) / 2 + (j - i - 1);
+}
+constexpr double RSQRT2 = 0.70710678118654752440;
+constexpr int NS = 15, NA = 10;
+
+// Build U = exp(L(g) g.dt) for every point of the block (block-uniform control
+// flow; lane (pl, j) computes one Chebyshev column, then one output tile per
+// squaring) and return this lane's row j of U (full 25-coordinate form) in u.
+// Without SYM, U[p] holds the 25x25 matrix; with SYM its first 325 doubles hold
+// Us (15x15, row-major) then Ua (10x10).
 template <bool SYM>
 __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& s_max, const PointP& q,
                                                  const Seg& g, bool valid, bool lane_ok, int t, int pl,
                                                  int j, double& nuse, double& nexec, double& nsq,
-                                                 bool& over_cap) {
-  const int rb = j / 5, cb = j % 5;
+                                                 bool& over_cap, double (&u)[NC]) {
   double rsum = 0.0;
 #pragma unroll
   for (int c = 0; c < 4; ++c) rsum += fabs(q.gA[c]) + fabs(q.gB[c]);
@@ -671,6 +696,7 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
   const bool capped = valid && !(x <= 1e12);
   const bool active = valid && !capped && x > X_SKIP && lane_ok;
   over_cap = over_cap || capped;
+  constexpr double X_BASE = SYM ? X_BASE_SYM : X_BASE_FULL;
   int sq = 0;
   if (active && x > X_BASE) sq = (int)ceil(log2(x / X_BASE));
   const double y = active ? ldexp(x, -sq) : 0.0;
@@ -678,54 +704,121 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
   const Gen A = make_gen(g, q.d1, q.gA, sc);
   const Gen B = make_gen(g, q.d1, q.gB, sc);
   const double vs = sc * 0.5 * q.V;
-  // (1) column j of exp(y Y)
+  // SYM: lane j < 15 starts from sym_j, lane 15 + a from asym_a; else from e_j
+  int bi = 0, bj = 0;                       // basis pair (bi <= bj)
+  if (SYM) {
+    if (j < NS) {
+      while (sym_index(bi, 4) < j) ++bi;
+      bj = bi + (j - sym_index(bi, bi));
+    } else {
+      while (bi < 3 && asym_index(bi, 4) < j - NS) ++bi;
+      bj = bi + 1 + (j - NS - asym_index(bi, bi + 1));
+    }
+  }
+  const bool is_sym = j < NS;
+  const double w0 = SYM ? ((bi == bj) ? 1.0 : RSQRT2) : 1.0;
+  const int e1 = SYM ? 5 * bi + bj : j, e2 = SYM ? 5 * bj + bi : j;
+  const double w2 = SYM ? (is_sym ? w0 : -w0) : 0.0;
+  // (1) column of exp(y Y)
   double v[25];
 #pragma unroll
-  for (int e = 0; e < 25; ++e) v[e] = (e == j) ? 1.0 : 0.0;
+  for (int e = 0; e < 25; ++e) v[e] = (e == e1) ? w0 : ((e == e2) ? w2 : 0.0);
   cheb_segment<25>(v, y, active,
                    [&](const double (&b)[25], double (&o)[25]) { apply_L<SYM>(A, B, vs, b, o); },
                    nuse, nexec);
   if (t == 0) s_max = 0;
   __syncthreads();
+  double* Ub = &U[pl][0][0];
   if (lane_ok) {
+    if (!SYM) {
 #pragma unroll
-    for (int r = 0; r < 25; ++r) U[pl][r][j] = v[r];
+      for (int r = 0; r < 25; ++r) U[pl][r][j] = v[r];
+    } else if (is_sym) {                    // Us[s'][j] = <sym_s', v>
+#pragma unroll
+      for (int i2 = 0; i2 < 5; ++i2)
+#pragma unroll
+        for (int j2 = i2; j2 < 5; ++j2)
+          Ub[sym_index(i2, j2) * NS + j] =
+              (i2 == j2) ? v[5 * i2 + i2] : RSQRT2 * (v[5 * i2 + j2] + v[5 * j2 + i2]);
+    } else {                                // Ua[a'][j-15] = <asym_a', v>
+#pragma unroll
+      for (int i2 = 0; i2 < 5; ++i2)
+#pragma unroll
+        for (int j2 = i2 + 1; j2 < 5; ++j2)
+          Ub[NS * NS + asym_index(i2, j2) * NA + (j - NS)] = RSQRT2 * (v[5 * i2 + j2] - v[5 * j2 + i2]);
+    }
     atomicMax(&s_max, sq);
   }
   __syncthreads();
   const int smx = s_max;
   nsq += (double)sq;
-  // (2) squarings: tile (rb, cb) of U U
+  // (2) squarings.  Full: lane owns the 5x5 tile (j/5, j%5) of U U.  SYM: lanes
+  // 0-14 own 5x3 tiles of Us (K = 15), lanes 15-24 own 5x2 tiles of Ua (K = 10),
+  // all with one code path (3 columns; a 5x2 tile repeats its last column).
+  const int ld = SYM ? (is_sym ? NS : NA) : NC;
+  const int nk = ld;
+  const int boff = SYM ? (is_sym ? 0 : NS * NS) : 0;
+  const int r0 = SYM ? (is_sym ? 5 * (j / 5) : 5 * ((j - NS) / 5)) : 5 * (j / 5);
+  const int c0 = SYM ? (is_sym ? 3 * (j % 5) : 2 * ((j - NS) % 5)) : 5 * (j % 5);
+  const int ncol = SYM ? (is_sym ? 3 : 2) : 5;
+  constexpr int TC = SYM ? 3 : 5;           // tile columns held per lane
+  const double* Mb = Ub + boff;
   for (int it = 0; it < smx; ++it) {
-    double acc[5][5];
+    double acc[5][TC];
 #pragma unroll
     for (int a = 0; a < 5; ++a)
 #pragma unroll
-      for (int b = 0; b < 5; ++b) acc[a][b] = 0.0;
+      for (int b = 0; b < TC; ++b) acc[a][b] = 0.0;
     if (lane_ok && it < sq) {
 #ifdef RYD_SQ_UNROLL
 #pragma unroll RYD_SQ_UNROLL
 #endif
-      for (int k = 0; k < NC; ++k) {
-        double ar[5], bc[5];
+      for (int k = 0; k < nk; ++k) {
+        double ar[5], bc[TC];
 #pragma unroll
-        for (int a = 0; a < 5; ++a) ar[a] = U[pl][5 * rb + a][k];
+        for (int a = 0; a < 5; ++a) ar[a] = Mb[(r0 + a) * ld + k];
 #pragma unroll
-        for (int b = 0; b < 5; ++b) bc[b] = U[pl][k][5 * cb + b];
+        for (int b = 0; b < TC; ++b) bc[b] = Mb[k * ld + c0 + (b < ncol ? b : ncol - 1)];
 #pragma unroll
         for (int a = 0; a < 5; ++a)
 #pragma unroll
-          for (int b = 0; b < 5; ++b) acc[a][b] = fma(ar[a], bc[b], acc[a][b]);
+          for (int b = 0; b < TC; ++b) acc[a][b] = fma(ar[a], bc[b], acc[a][b]);
       }
     }
     __syncthreads();
     if (lane_ok && it < sq) {
+      double* Mw = Ub + boff;
 #pragma unroll
       for (int a = 0; a < 5; ++a)
 #pragma unroll
-        for (int b = 0; b < 5; ++b) U[pl][5 * rb + a][5 * cb + b] = acc[a][b];
+        for (int b = 0; b < TC; ++b)
+          if (b < ncol) Mw[(r0 + a) * ld + c0 + b] = acc[a][b];
     }
     __syncthreads();
+  }
+  // (3) this lane's row of U in full coordinates
+  if (!SYM) {
+#pragma unroll
+    for (int m = 0; m < NC; ++m) u[m] = U[pl][j][m];
+  } else {
+    const int ra = j / 5, rb = j % 5;
+    const int lo = ra < rb ? ra : rb, hi = ra < rb ? rb : ra;
+    const int sr = sym_index(lo, hi);
+    const double wsr = (ra == rb) ? 1.0 : RSQRT2;
+    const int ar_ = (ra == rb) ? 0 : asym_index(lo, hi);
+    const double war = (ra == rb) ? 0.0 : (ra < rb ? RSQRT2 : -RSQRT2);
+    const double* Us = Ub;
+    const double* Ua = Ub + NS * NS;
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+      const int ca = m / 5, cb = m % 5;
+      const int clo = ca < cb ? ca : cb, chi = ca < cb ? cb : ca;
+      const double wsc = (ca == cb) ? 1.0 : RSQRT2;
+      const double wac = (ca == cb) ? 0.0 : (ca < cb ? RSQRT2 : -RSQRT2);
+      double val = wsr * wsc * Us[sr * NS + sym_index(clo, chi)];
+      if (ca != cb) val = fma(war * wac, Ua[ar_ * NA + asym_index(clo, chi)], val);
+      u[m] = val;
+    }
   }
 }
 
@@ -781,7 +874,9 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
   const int nseg = n_segments<PROTO>(n_steps);
   const bool use_frame = phase_frame_protocol<PROTO>() && __syncthreads_and(frame_ok || !lane_ok);
 
-  // one propagator per segment, or a single phase-0 propagator in the frame path
+  // one propagator per segment, or a single phase-0 propagator in the frame path;
+  // u = this lane's row of the latest propagator
+  double u[NC];
   const int nprop = use_frame ? 1 : nseg;
   for (int s = 0; s < nprop; ++s) {
     // re-read this point's scalars every segment (L1/L2 hits) instead of keeping
@@ -794,15 +889,15 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
       g.om_re = q.Om;
       g.om_im = 0.0;
     }
-    build_propagator<SYM>(U, s_max, q, g, valid, lane_ok, t, pl, j, nuse, nexec, nsq, over_cap);
+    build_propagator<SYM>(U, s_max, q, g, valid, lane_ok, t, pl, j, nuse, nexec, nsq, over_cap, u);
     if (!use_frame) {
       // R_k <- U R_k ; lane (pl, r = j) computes row r for the 4 inputs
       double nr[4] = {0.0, 0.0, 0.0, 0.0};
       if (lane_ok) {
-        for (int m = 0; m < NC; ++m) {
-          const double u = U[pl][j][m];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) nr[k] = fma(u, Rs[pl][k][m], nr[k]);
+        for (int m = 0; m < NC; ++m) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) nr[k] = fma(u[m], Rs[pl][k][m], nr[k]);
         }
       }
       __syncthreads();
@@ -816,9 +911,6 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
 
   if (use_frame) {
     // U0 row j stays in registers for every segment
-    double u[NC];
-#pragma unroll
-    for (int m = 0; m < NC; ++m) u[m] = U[pl][j][m];
     double cp = 1.0, sp = 0.0;               // phase of the frame R is currently in
     for (int s = 0; s < nseg; ++s) {
       const double* pp = prm;
@@ -1106,6 +1198,206 @@ __global__ __launch_bounds__(DP_BLOCK) void lindblad_dopri5_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Coherence sectors of the qubit process map
+// ---------------------------------------------------------------------------
+// Single-atom operators |i><j| carry q = n(i) - n(j), n(0) = 0, n(1) = n(r) = 1.
+// H and every collapse channel conserve q, so the 16 qubit matrix units evolve in
+// small invariant sectors of the two-atom operator space (C[alpha][beta] below,
+// alpha over atom A's sector basis, beta over atom B's):
+//   (0,0)   |x><x|               real 25-dim sector: the kernels above
+//   KIND 0 (0,-1)  |00><01|, |10><11|   A: q=0 {e00,e11,err,ex,ey}, B: q=-1 {|0><1|, |0><r|}
+//   KIND 1 (-1,0)  |00><10|, |01><11|   mirror
+//   KIND 2 (-1,-1) |00><11|             A, B: q=-1
+//   KIND 3 (-1,+1) |01><10|             A: q=-1, B: q=+1 {|1><0|, |r><0|}; V drops out
+// q=0 block: the real single-atom M above, acting on complex coefficients.
+// q=-1 block: d/dt (c01, c0r) = [[i d1 - gs/2, i Om/2], [i Om*/2, -i Delta - (g0+g1+gphi)/2]]
+// q=+1 block: its complex conjugate.  V term (V/2)(S (x) D + D (x) S) with S = diag(0,1)
+// and D = +-i diag(0,1) on q = -+1 (S, D on q=0 as in apply_V).  The other 6 matrix
+// units are adjoints of these.  Verified against the column-stacked 81x81 Liouvillian
+// (tests/test_gpu_process_map.py).
+struct CGen {                  // scaled complex 2x2 block
+  double m00r, m00i, m01r, m01i, m10r, m10i, m11r, m11i;
+};
+
+__device__ __forceinline__ CGen make_cgen(const Seg& g, double d1, const double* r, double s, bool conj) {
+  CGen c;
+  const double sg = conj ? -1.0 : 1.0;
+  c.m00r = -0.5 * s * r[3];
+  c.m00i = sg * s * d1;
+  c.m01r = -0.5 * s * g.om_im;                   // i Om/2 (conj: imaginary parts flip)
+  c.m01i = sg * (0.5 * s * g.om_re);
+  c.m10r = 0.5 * s * g.om_im;                    // i Om*/2
+  c.m10i = sg * (0.5 * s * g.om_re);
+  c.m11r = -0.5 * s * (r[0] + r[1] + r[2]);
+  c.m11i = -sg * s * g.dl;
+  return c;
+}
+
+// complex o += m z
+#define CMAC(or_, oi, mr, mi, zr, zi) \
+  do {                                 \
+    or_ = fma(mr, zr, or_);            \
+    or_ = fma(-(mi), zi, or_);         \
+    oi = fma(mr, zi, oi);              \
+    oi = fma(mi, zr, oi);              \
+  } while (0)
+
+// o[0..4] += M0 u[0..4] for one (re or im) component, stride-addressed
+template <int ST>
+__device__ __forceinline__ void m0_apply(const Gen& a, const double* b, double* o) {
+  const double u1 = b[1 * ST], u2 = b[2 * ST], u3 = b[3 * ST], u4 = b[4 * ST];
+  o[0] = fma(a.g0, u2, o[0]);
+  o[1 * ST] = fma(a.g1, u2, fma(a.hy2, u3, fma(-a.hx2, u4, o[1 * ST])));
+  o[2 * ST] = fma(a.mg01, u2, fma(-a.hy2, u3, fma(a.hx2, u4, o[2 * ST])));
+  o[3 * ST] = fma(a.hy, u2 - u1, fma(-a.G, u3, fma(a.hz2, u4, o[3 * ST])));
+  o[4 * ST] = fma(a.hx, u1 - u2, fma(-a.hz2, u3, fma(-a.G, u4, o[4 * ST])));
+}
+
+// o += 2Y b on a coherence sector; complex C[alpha][beta] interleaved (re, im)
+template <int KIND>
+__device__ __forceinline__ void apply_coh(const Gen& A0, const Gen& B0, const CGen& Am, const CGen& Bm,
+                                          double vs, const double* b, double* o) {
+  if (KIND == 0) {                 // C[5][2]: index 2*alpha + beta
+    // A (q=0) on alpha, each beta and re/im: stride 4 doubles
+#pragma unroll
+    for (int be = 0; be < 2; ++be)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) m0_apply<4>(A0, b + 2 * be + c, o + 2 * be + c);
+    // B (q=-1) on beta
+#pragma unroll
+    for (int al = 0; al < 5; ++al) {
+      const double z0r = b[4 * al], z0i = b[4 * al + 1], z1r = b[4 * al + 2], z1i = b[4 * al + 3];
+      CMAC(o[4 * al], o[4 * al + 1], Bm.m00r, Bm.m00i, z0r, z0i);
+      CMAC(o[4 * al], o[4 * al + 1], Bm.m01r, Bm.m01i, z1r, z1i);
+      CMAC(o[4 * al + 2], o[4 * al + 3], Bm.m10r, Bm.m10i, z0r, z0i);
+      CMAC(o[4 * al + 2], o[4 * al + 3], Bm.m11r, Bm.m11i, z1r, z1i);
+    }
+    // V: S_A (x) (i on beta=1): alpha = err (x2), ex, ey ; D_A (x) S_B: ex -> ey, ey -> -ex on beta=1
+#pragma unroll
+    for (int al = 2; al < 5; ++al) {
+      const double sa = (al == 2) ? 2.0 * vs : vs;
+      o[4 * al + 2] = fma(-sa, b[4 * al + 3], o[4 * al + 2]);
+      o[4 * al + 3] = fma(sa, b[4 * al + 2], o[4 * al + 3]);
+    }
+    o[4 * 4 + 2] = fma(vs, b[4 * 3 + 2], o[4 * 4 + 2]);
+    o[4 * 4 + 3] = fma(vs, b[4 * 3 + 3], o[4 * 4 + 3]);
+    o[4 * 3 + 2] = fma(-vs, b[4 * 4 + 2], o[4 * 3 + 2]);
+    o[4 * 3 + 3] = fma(-vs, b[4 * 4 + 3], o[4 * 3 + 3]);
+  } else if (KIND == 1) {          // C[2][5]: index 5*alpha + beta
+#pragma unroll
+    for (int al = 0; al < 2; ++al)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) m0_apply<2>(B0, b + 10 * al + c, o + 10 * al + c);
+#pragma unroll
+    for (int be = 0; be < 5; ++be) {
+      const double z0r = b[2 * be], z0i = b[2 * be + 1], z1r = b[10 + 2 * be], z1i = b[10 + 2 * be + 1];
+      CMAC(o[2 * be], o[2 * be + 1], Am.m00r, Am.m00i, z0r, z0i);
+      CMAC(o[2 * be], o[2 * be + 1], Am.m01r, Am.m01i, z1r, z1i);
+      CMAC(o[10 + 2 * be], o[10 + 2 * be + 1], Am.m10r, Am.m10i, z0r, z0i);
+      CMAC(o[10 + 2 * be], o[10 + 2 * be + 1], Am.m11r, Am.m11i, z1r, z1i);
+    }
+    // V: S_A(alpha=1) (x) D_B: ex -> ey, ey -> -ex ; D_A (i on alpha=1) (x) S_B
+    o[10 + 2 * 4] = fma(vs, b[10 + 2 * 3], o[10 + 2 * 4]);
+    o[10 + 2 * 4 + 1] = fma(vs, b[10 + 2 * 3 + 1], o[10 + 2 * 4 + 1]);
+    o[10 + 2 * 3] = fma(-vs, b[10 + 2 * 4], o[10 + 2 * 3]);
+    o[10 + 2 * 3 + 1] = fma(-vs, b[10 + 2 * 4 + 1], o[10 + 2 * 3 + 1]);
+#pragma unroll
+    for (int be = 2; be < 5; ++be) {
+      const double sb = (be == 2) ? 2.0 * vs : vs;
+      o[10 + 2 * be] = fma(-sb, b[10 + 2 * be + 1], o[10 + 2 * be]);
+      o[10 + 2 * be + 1] = fma(sb, b[10 + 2 * be], o[10 + 2 * be + 1]);
+    }
+  } else {                         // C[2][2]: index 2*alpha + beta; A q=-1, B q=-1 or q=+1
+#pragma unroll
+    for (int be = 0; be < 2; ++be) {
+      const double z0r = b[2 * be], z0i = b[2 * be + 1], z1r = b[4 + 2 * be], z1i = b[4 + 2 * be + 1];
+      CMAC(o[2 * be], o[2 * be + 1], Am.m00r, Am.m00i, z0r, z0i);
+      CMAC(o[2 * be], o[2 * be + 1], Am.m01r, Am.m01i, z1r, z1i);
+      CMAC(o[4 + 2 * be], o[4 + 2 * be + 1], Am.m10r, Am.m10i, z0r, z0i);
+      CMAC(o[4 + 2 * be], o[4 + 2 * be + 1], Am.m11r, Am.m11i, z1r, z1i);
+    }
+#pragma unroll
+    for (int al = 0; al < 2; ++al) {
+      const double z0r = b[4 * al], z0i = b[4 * al + 1], z1r = b[4 * al + 2], z1i = b[4 * al + 3];
+      CMAC(o[4 * al], o[4 * al + 1], Bm.m00r, Bm.m00i, z0r, z0i);
+      CMAC(o[4 * al], o[4 * al + 1], Bm.m01r, Bm.m01i, z1r, z1i);
+      CMAC(o[4 * al + 2], o[4 * al + 3], Bm.m10r, Bm.m10i, z0r, z0i);
+      CMAC(o[4 * al + 2], o[4 * al + 3], Bm.m11r, Bm.m11i, z1r, z1i);
+    }
+    if (KIND == 2) {               // (S (x) D + D (x) S) on C[1][1]: i + i
+      o[6] = fma(-2.0 * vs, b[7], o[6]);
+      o[7] = fma(2.0 * vs, b[6], o[7]);
+    }
+  }
+}
+
+template <int PROTO, int KIND>
+__global__ __launch_bounds__(BLOCK) void coherence_cheb_kernel(
+    const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ out, int64_t ldo,
+    uint32_t* __restrict__ status, int n_steps, int shape) {
+  constexpr int NIN = KIND < 2 ? 2 : 1;     // inputs of this sector per point
+  constexpr int NV = KIND < 2 ? 20 : 8;
+  const int64_t gid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = gid < NIN * n;
+  const int64_t i = live ? gid / NIN : (n - 1);
+  const int sub = (int)(gid % NIN);
+  const PointP q = load_point<PROTO>(prm, ldp, i);
+  const bool valid = point_valid<PROTO>(q, n_steps);
+  // start: KIND 0 C[sub][0] (|00><01|: e00 (x) |0><1| ; |10><11|: e11 (x) |0><1|),
+  //        KIND 1 C[0][sub], KIND 2/3 C[0][0]
+  const int e0 = KIND == 0 ? 4 * sub : (KIND == 1 ? 2 * sub : 0);
+  double v[NV];
+#pragma unroll
+  for (int e = 0; e < NV; ++e) v[e] = (e == e0) ? 1.0 : 0.0;
+  double nuse = 0.0, nexec = 0.0;
+  bool over_cap = false;
+  const int nseg = n_segments<PROTO>(n_steps);
+  double rsum = 0.0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) rsum += fabs(q.gA[c]) + fabs(q.gB[c]);
+  for (int s = 0; s < nseg; ++s) {
+    const Seg g = segment<PROTO>(q, s, n_steps, shape);
+    double emin, emax;
+    h_bounds(g, q.V, q.d1, emin, emax);
+    const double omega = (emax - emin) + rsum;
+    const double x = omega * g.dt;
+    const bool capped = valid && !(x <= X_CAP);
+    const bool active = valid && !capped && x > X_SKIP;
+    over_cap = over_cap || capped;
+    const double sc = active ? 2.0 / omega : 0.0;
+    const Gen A0 = make_gen(g, q.d1, q.gA, sc);
+    const Gen B0 = make_gen(g, q.d1, q.gB, sc);
+    const CGen Am = make_cgen(g, q.d1, q.gA, sc, false);
+    const CGen Bm = make_cgen(g, q.d1, q.gB, sc, KIND == 3);
+    const double vs = sc * 0.5 * q.V;
+    cheb_segment<NV>(v, x, active,
+                     [&](const double (&b)[NV], double (&o)[NV]) { apply_coh<KIND>(A0, B0, Am, Bm, vs, b, o); },
+                     nuse, nexec);
+  }
+  uint32_t stat = valid ? 0u : RYD_STATUS_BAD_INPUT;
+  if (over_cap) stat |= RYD_STATUS_STEP_CAP;
+  if (!finite_all(v, NV)) stat |= RYD_STATUS_NONFINITE;
+  if (!live) return;
+  // qubit-block images: KIND 0 o0 = C[0][0] (|00><01|), o1 = C[1][0] (|10><11|);
+  // KIND 1 o0 = C[0][0] (|00><10|), o1 = C[0][1] (|01><11|); KIND 2/3 C[0][0]
+  if (KIND < 2) {
+    const int base = (KIND == 0 ? RYD_C_K0 : RYD_C_K1) + 4 * sub;
+    const int i1 = KIND == 0 ? 4 : 2;
+    out[(int64_t)(base + 0) * ldo + i] = v[0];
+    out[(int64_t)(base + 1) * ldo + i] = v[1];
+    out[(int64_t)(base + 2) * ldo + i] = v[i1];
+    out[(int64_t)(base + 3) * ldo + i] = v[i1 + 1];
+  } else {
+    const int base = KIND == 2 ? RYD_C_K2 : RYD_C_K3;
+    out[(int64_t)(base + 0) * ldo + i] = v[0];
+    out[(int64_t)(base + 1) * ldo + i] = v[1];
+  }
+  if (stat) atomicOr(&status[i], stat);
+  (void)nuse;
+  (void)nexec;
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 thread_local std::string g_err;
@@ -1232,12 +1524,165 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
   return RYD_OK;
 }
 
-}  // namespace
+template <int PROTO>
+int launch_coherences_proto(const double* dp, int64_t n, int64_t ldp, double* dc, int64_t ldc,
+                            uint32_t* dstat, int ns, int sh, hipStream_t stream) {
+  using CFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, uint32_t*, int, int);
+  const CFn fns[4] = {coherence_cheb_kernel<PROTO, 0>, coherence_cheb_kernel<PROTO, 1>,
+                      coherence_cheb_kernel<PROTO, 2>, coherence_cheb_kernel<PROTO, 3>};
+  for (int k = 0; k < 4; ++k) {
+    const int64_t lanes = (k < 2 ? 2 : 1) * n;
+    const int64_t blocks = (lanes + BLOCK - 1) / BLOCK;
+    if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
+    void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&dc, (void*)&ldc,
+                    (void*)&dstat, (void*)&ns, (void*)&sh};
+    HIPCHK(hipLaunchKernel((const void*)fns[k], dim3((unsigned)blocks), dim3(BLOCK), args, 0, stream));
+  }
+  return RYD_OK;
+}
 
-struct ryd_handle {
-  std::vector<int> dev;
-  std::vector<hipStream_t> stream;
+// The four coherence-sector launches of one batch; status is cleared first and
+// each kernel ORs its bits in.
+int launch_coherences(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, double* dc,
+                      int64_t ldc, uint32_t* dstat, hipStream_t stream) {
+  if (n == 0) return RYD_OK;
+  HIPCHK(hipMemsetAsync(dstat, 0, sizeof(uint32_t) * n, stream));
+  switch (d->protocol) {
+    case RYD_PROTO_LP_SQUARE:
+      return launch_coherences_proto<RYD_PROTO_LP_SQUARE>(dp, n, ldp, dc, ldc, dstat, d->n_steps, d->shape, stream);
+    case RYD_PROTO_LP_SHAPED:
+      return launch_coherences_proto<RYD_PROTO_LP_SHAPED>(dp, n, ldp, dc, ldc, dstat, d->n_steps, d->shape, stream);
+    case RYD_PROTO_BANGBANG:
+      return launch_coherences_proto<RYD_PROTO_BANGBANG>(dp, n, ldp, dc, ldc, dstat, d->n_steps, d->shape, stream);
+    default:
+      return launch_coherences_proto<RYD_PROTO_SMOOTH_JP>(dp, n, ldp, dc, ldc, dstat, d->n_steps, d->shape, stream);
+  }
+}
+
+int validate_coherences(const ryd_batch_desc* d, int64_t n, int64_t ldp, int64_t ldc) {
+  if (!d) return fail(RYD_ERR_INVALID, "desc is NULL");
+  ryd_batch_desc v = *d;                   // the Chebyshev vector method, Lindblad bookkeeping
+  v.method = RYD_METHOD_CHEB_VECTOR;
+  v.evolution = RYD_EVOL_LINDBLAD;
+  int rc = validate(&v, n, ldp, 4 * n, n);
+  if (rc) return rc;
+  if (ldc < n) return fail(RYD_ERR_INVALID, "leading dimension too small");
+  return RYD_OK;
+}
+
+// One output array of a partitioned run: `rows` rows of `per_point` doubles per point.
+struct HostOut {
+  double* host;
+  int64_t ld;
+  int rows;
+  int per_point;
 };
+
+// Range-partition n points over the handle's devices (point i -> device
+// floor(nd*i/n)), one stream each, no inter-device traffic:
+// gather params, run `launch_fn(dp, cnt, ldp, dev_outs, dstat, stream)`, scatter
+// outputs, wait for all.  Device times are the max over devices.
+template <typename LaunchFn>
+int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_params,
+                    const std::vector<HostOut>& outs, uint32_t* out_status, LaunchFn launch_fn,
+                    double& kms, double& hms, double& dms) {
+  const int nd = (int)h->dev.size();
+  const int no = (int)outs.size();
+  struct Part {
+    int64_t off, cnt;
+    double* p;
+    std::vector<double*> o;
+    uint32_t* st;
+    hipEvent_t a, b, c, d;
+    bool ev;
+  };
+  std::vector<Part> parts(nd);
+  for (int k = 0; k < nd; ++k) {
+    parts[k].off = n * k / nd;
+    parts[k].cnt = n * (k + 1) / nd - parts[k].off;
+    parts[k].p = nullptr;
+    parts[k].o.assign(no, nullptr);
+    parts[k].st = nullptr;
+    parts[k].ev = false;
+  }
+  auto cleanup = [&]() {
+    for (int k = 0; k < nd; ++k) {
+      Part& P = parts[k];
+      (void)hipSetDevice(h->dev[k]);
+      (void)hipStreamSynchronize(h->stream[k]);
+      if (P.p) (void)hipFree(P.p);
+      for (auto& q : P.o)
+        if (q) (void)hipFree(q);
+      if (P.st) (void)hipFree(P.st);
+      if (P.ev) {
+        (void)hipEventDestroy(P.a);
+        (void)hipEventDestroy(P.b);
+        (void)hipEventDestroy(P.c);
+        (void)hipEventDestroy(P.d);
+      }
+      P.p = nullptr;
+      P.o.assign(no, nullptr);
+      P.st = nullptr;
+      P.ev = false;
+    }
+  };
+  kms = hms = dms = 0.0;
+  for (int k = 0; k < nd; ++k) {
+    Part& P = parts[k];
+    if (P.cnt == 0) continue;
+    (void)hipSetDevice(h->dev[k]);
+    hipStream_t s = h->stream[k];
+    bool ok = hipMalloc(&P.p, sizeof(double) * RYD_NPARAM * P.cnt) == hipSuccess &&
+              hipMalloc(&P.st, sizeof(uint32_t) * P.cnt) == hipSuccess;
+    for (int j = 0; j < no && ok; ++j)
+      ok = hipMalloc(&P.o[j], sizeof(double) * outs[j].rows * outs[j].per_point * P.cnt) == hipSuccess;
+    if (!ok) {
+      cleanup();
+      return fail(RYD_ERR_ALLOC, "device allocation failed");
+    }
+    P.ev = hipEventCreate(&P.a) == hipSuccess && hipEventCreate(&P.b) == hipSuccess &&
+           hipEventCreate(&P.c) == hipSuccess && hipEventCreate(&P.d) == hipSuccess;
+    if (!P.ev) {
+      cleanup();
+      return fail(RYD_ERR_HIP, "event creation failed");
+    }
+    (void)hipEventRecord(P.a, s);
+    // gather this shard's SoA columns
+    (void)hipMemcpy2DAsync(P.p, sizeof(double) * P.cnt, params + P.off, sizeof(double) * ld_params,
+                           sizeof(double) * P.cnt, RYD_NPARAM, hipMemcpyHostToDevice, s);
+    (void)hipEventRecord(P.b, s);
+    int rc = launch_fn(P.p, P.cnt, P.cnt, P.o, P.st, s);
+    if (rc) {
+      cleanup();
+      return rc;
+    }
+    (void)hipEventRecord(P.c, s);
+    for (int j = 0; j < no; ++j) {
+      const int64_t w = (int64_t)outs[j].per_point * P.cnt;
+      (void)hipMemcpy2DAsync(outs[j].host + outs[j].per_point * P.off, sizeof(double) * outs[j].ld, P.o[j],
+                             sizeof(double) * w, sizeof(double) * w, outs[j].rows, hipMemcpyDeviceToHost, s);
+    }
+    (void)hipMemcpyAsync(out_status + P.off, P.st, sizeof(uint32_t) * P.cnt, hipMemcpyDeviceToHost, s);
+    (void)hipEventRecord(P.d, s);
+  }
+  hipError_t err = hipSuccess;
+  for (int k = 0; k < nd; ++k) {
+    Part& P = parts[k];
+    if (P.cnt == 0) continue;
+    (void)hipSetDevice(h->dev[k]);
+    hipError_t e = hipStreamSynchronize(h->stream[k]);
+    if (e != hipSuccess) err = e;
+    float t;
+    if (hipEventElapsedTime(&t, P.a, P.b) == hipSuccess) hms = fmax(hms, t);
+    if (hipEventElapsedTime(&t, P.b, P.c) == hipSuccess) kms = fmax(kms, t);
+    if (hipEventElapsedTime(&t, P.c, P.d) == hipSuccess) dms = fmax(dms, t);
+  }
+  cleanup();
+  if (err != hipSuccess) return fail(RYD_ERR_HIP, std::string("batch: ") + hipGetErrorString(err));
+  return RYD_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -1278,7 +1723,7 @@ int ryd_create(const int* device_ids, int n_devices, ryd_handle** out) {
     hipError_t e = hipSetDevice(d);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e != hipSuccess) {
-      for (size_t j = 0; j < h->stream.size(); ++j) hipStreamDestroy(h->stream[j]);
+      for (size_t j = 0; j < h->stream.size(); ++j) (void)hipStreamDestroy(h->stream[j]);
       delete h;
       return fail(RYD_ERR_HIP, std::string("stream create: ") + hipGetErrorString(e));
     }
@@ -1291,9 +1736,9 @@ int ryd_create(const int* device_ids, int n_devices, ryd_handle** out) {
 int ryd_destroy(ryd_handle* h) {
   if (!h) return RYD_OK;
   for (size_t k = 0; k < h->dev.size(); ++k) {
-    hipSetDevice(h->dev[k]);
-    hipStreamSynchronize(h->stream[k]);
-    hipStreamDestroy(h->stream[k]);
+    (void)hipSetDevice(h->dev[k]);
+    (void)hipStreamSynchronize(h->stream[k]);
+    (void)hipStreamDestroy(h->stream[k]);
   }
   delete h;
   return RYD_OK;
@@ -1360,8 +1805,8 @@ int ryd_run_batch_device(ryd_handle* h, int slot, const ryd_batch_desc* desc, co
     HIPCHK(hipEventRecord(e1, s));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(elapsed_ms, e0, e1));
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
   }
   return RYD_OK;
 }
@@ -1374,87 +1819,15 @@ int ryd_run_batch(ryd_handle* h, const ryd_batch_desc* desc, const double* param
   if (rc) return rc;
   if (n > 0 && (!params || !out_state || !out_summary || !out_status))
     return fail(RYD_ERR_INVALID, "NULL buffer");
-  const int nd = (int)h->dev.size();
   const int sw = ryd_state_width(desc->evolution, desc->dim);
-  struct Part {
-    int64_t off, cnt;
-    double *p, *s, *m;
-    uint32_t* st;
-    hipEvent_t a, b, c, d;
-  };
-  std::vector<Part> parts(nd);
-  // contiguous range shards, point i -> device floor(nd*i/n)
-  for (int k = 0; k < nd; ++k) {
-    parts[k].off = n * k / nd;
-    parts[k].cnt = n * (k + 1) / nd - parts[k].off;
-    parts[k].p = parts[k].s = parts[k].m = nullptr;
-    parts[k].st = nullptr;
-  }
-  auto cleanup = [&]() {
-    for (int k = 0; k < nd; ++k) {
-      hipSetDevice(h->dev[k]);
-      hipStreamSynchronize(h->stream[k]);
-      if (parts[k].p) hipFree(parts[k].p);
-      if (parts[k].s) hipFree(parts[k].s);
-      if (parts[k].m) hipFree(parts[k].m);
-      if (parts[k].st) hipFree(parts[k].st);
-      parts[k].p = parts[k].s = parts[k].m = nullptr;
-      parts[k].st = nullptr;
-    }
-  };
-  double kms = 0.0, hms = 0.0, dms = 0.0;
-  for (int k = 0; k < nd; ++k) {
-    Part& P = parts[k];
-    if (P.cnt == 0) continue;
-    hipSetDevice(h->dev[k]);
-    hipStream_t s = h->stream[k];
-    if (hipMalloc(&P.p, sizeof(double) * RYD_NPARAM * P.cnt) != hipSuccess ||
-        hipMalloc(&P.s, sizeof(double) * sw * 4 * P.cnt) != hipSuccess ||
-        hipMalloc(&P.m, sizeof(double) * RYD_NSUMMARY * P.cnt) != hipSuccess ||
-        hipMalloc(&P.st, sizeof(uint32_t) * P.cnt) != hipSuccess) {
-      cleanup();
-      return fail(RYD_ERR_ALLOC, "device allocation failed");
-    }
-    hipEventCreate(&P.a);
-    hipEventCreate(&P.b);
-    hipEventCreate(&P.c);
-    hipEventCreate(&P.d);
-    hipEventRecord(P.a, s);
-    // gather this shard's SoA columns
-    hipMemcpy2DAsync(P.p, sizeof(double) * P.cnt, params + P.off, sizeof(double) * ld_params,
-                     sizeof(double) * P.cnt, RYD_NPARAM, hipMemcpyHostToDevice, s);
-    hipEventRecord(P.b, s);
-    rc = launch(desc, P.p, P.cnt, P.cnt, P.s, 4 * P.cnt, P.m, P.cnt, P.st, s);
-    if (rc) {
-      cleanup();
-      return rc;
-    }
-    hipEventRecord(P.c, s);
-    hipMemcpy2DAsync(out_state + 4 * P.off, sizeof(double) * ld_state, P.s, sizeof(double) * 4 * P.cnt,
-                     sizeof(double) * 4 * P.cnt, sw, hipMemcpyDeviceToHost, s);
-    hipMemcpy2DAsync(out_summary + P.off, sizeof(double) * ld_summary, P.m, sizeof(double) * P.cnt,
-                     sizeof(double) * P.cnt, RYD_NSUMMARY, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(out_status + P.off, P.st, sizeof(uint32_t) * P.cnt, hipMemcpyDeviceToHost, s);
-    hipEventRecord(P.d, s);
-  }
-  hipError_t err = hipSuccess;
-  for (int k = 0; k < nd; ++k) {
-    Part& P = parts[k];
-    if (P.cnt == 0) continue;
-    hipSetDevice(h->dev[k]);
-    hipError_t e = hipStreamSynchronize(h->stream[k]);
-    if (e != hipSuccess) err = e;
-    float t;
-    if (hipEventElapsedTime(&t, P.a, P.b) == hipSuccess) hms = fmax(hms, t);
-    if (hipEventElapsedTime(&t, P.b, P.c) == hipSuccess) kms = fmax(kms, t);
-    if (hipEventElapsedTime(&t, P.c, P.d) == hipSuccess) dms = fmax(dms, t);
-    hipEventDestroy(P.a);
-    hipEventDestroy(P.b);
-    hipEventDestroy(P.c);
-    hipEventDestroy(P.d);
-  }
-  cleanup();
-  if (err != hipSuccess) return fail(RYD_ERR_HIP, std::string("batch: ") + hipGetErrorString(err));
+  const std::vector<HostOut> outs = {{out_state, ld_state, sw, 4}, {out_summary, ld_summary, RYD_NSUMMARY, 1}};
+  double kms, hms, dms;
+  rc = run_partitioned(
+      h, params, n, ld_params, outs, out_status,
+      [&](const double* dp, int64_t cnt, int64_t ldp, const std::vector<double*>& o, uint32_t* dst,
+          hipStream_t s) { return launch(desc, dp, cnt, ldp, o[0], 4 * cnt, o[1], cnt, dst, s); },
+      kms, hms, dms);
+  if (rc) return rc;
   if (stats) {
     stats->kernel_ms = kms;
     stats->h2d_ms = hms;
@@ -1466,8 +1839,60 @@ int ryd_run_batch(ryd_handle* h, const ryd_batch_desc* desc, const double* param
     }
     stats->matvec_useful = u;
     stats->matvec_exec = x;
-    stats->n_devices = nd;
+    stats->n_devices = (int)h->dev.size();
     stats->reserved = 0;
+  }
+  return RYD_OK;
+}
+
+int ryd_run_coherences(ryd_handle* h, const ryd_batch_desc* desc, const double* params, int64_t n,
+                       int64_t ld_params, double* out_coh, int64_t ld_coh, uint32_t* out_status,
+                       ryd_stats* stats) {
+  if (!h) return fail(RYD_ERR_INVALID, "handle is NULL");
+  int rc = validate_coherences(desc, n, ld_params, ld_coh);
+  if (rc) return rc;
+  if (n > 0 && (!params || !out_coh || !out_status)) return fail(RYD_ERR_INVALID, "NULL buffer");
+  const std::vector<HostOut> outs = {{out_coh, ld_coh, RYD_NCOH, 1}};
+  double kms, hms, dms;
+  rc = run_partitioned(
+      h, params, n, ld_params, outs, out_status,
+      [&](const double* dp, int64_t cnt, int64_t ldp, const std::vector<double*>& o, uint32_t* dst,
+          hipStream_t s) { return launch_coherences(desc, dp, cnt, ldp, o[0], cnt, dst, s); },
+      kms, hms, dms);
+  if (rc) return rc;
+  if (stats) {
+    stats->kernel_ms = kms;
+    stats->h2d_ms = hms;
+    stats->d2h_ms = dms;
+    stats->matvec_useful = stats->matvec_exec = 0.0;
+    stats->n_devices = (int)h->dev.size();
+    stats->reserved = 0;
+  }
+  return RYD_OK;
+}
+
+int ryd_run_coherences_device(ryd_handle* h, int slot, const ryd_batch_desc* desc, const double* d_params,
+                              int64_t n, int64_t ld_params, double* d_coh, int64_t ld_coh,
+                              uint32_t* d_status, void* stream, float* elapsed_ms) {
+  if (!h || slot < 0 || slot >= (int)h->dev.size()) return fail(RYD_ERR_INVALID, "bad handle/slot");
+  int rc = validate_coherences(desc, n, ld_params, ld_coh);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(h->dev[slot]));
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream[slot];
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (elapsed_ms) {
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+  }
+  rc = launch_coherences(desc, d_params, n, ld_params, d_coh, ld_coh, d_status, s);
+  if (rc) return rc;
+  if (elapsed_ms) {
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(elapsed_ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
   }
   return RYD_OK;
 }

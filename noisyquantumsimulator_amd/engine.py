@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -211,6 +211,26 @@ class Engine:
             status.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(st)))
         return EngineResult(evolution, n, state, summ, status, st.kernel_ms, st.h2d_ms, st.d2h_ms,
                             st.matvec_useful, st.matvec_exec)
+
+    def run_coherences(self, params: np.ndarray, protocol: str, n_steps: Optional[int] = None,
+                       shape: str = "square") -> Tuple[np.ndarray, np.ndarray]:
+        """The 6 upper off-diagonal qubit matrix units through the gate
+        (ryd_run_coherences): returns (coh (NCOH, n) float64, status (n,) uint32)."""
+        params = np.ascontiguousarray(params, dtype=np.float64)
+        if params.shape[0] != N.NPARAM:
+            raise ValueError(f"params must have shape ({N.NPARAM}, n)")
+        n = params.shape[1]
+        if n_steps is None:
+            n_steps = default_n_steps(protocol, params)
+        desc = make_desc(protocol, "lindblad", n_steps, shape, symmetric_atoms(params), "cheb_vector")
+        coh = np.zeros((N.NCOH, n), dtype=np.float64)
+        status = np.zeros(n, dtype=np.uint32)
+        st = N.Stats()
+        dptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        N.check(self.lib.ryd_run_coherences(
+            self.handle, ctypes.byref(desc), dptr(params), n, n, dptr(coh), n,
+            status.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(st)))
+        return coh, status
 
 
 class DeviceBatch:

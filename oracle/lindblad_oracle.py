@@ -412,3 +412,71 @@ def decay_kat(gamma: float, t: np.ndarray, method: str = "expm") -> np.ndarray:
         rho = evolve_state(H, psi, np.array([0.0, tt]), c, method=method)
         out.append(np.real(rho[1, 1]))
     return np.array(out)
+
+
+# --------------------------------------------------------------------------
+# qubit process map.  The reference's Kraus/CPTP extraction
+# (src/qpu_simulator/noise_models/__init__.py:1-22) is a stub, so there is no
+# reference oracle: these are the textbook definitions the build is checked
+# against, on the same exact propagators as run_point.
+# --------------------------------------------------------------------------
+
+QUBIT_INDEX = (0, 1, 3, 4)     # |00>, |01>, |10>, |11> in the dim-3 two-atom basis
+
+
+def process_map(p: PointSpec) -> np.ndarray:
+    """S[4c+d, 4a+b] = <c| E(|a><b|) |d>: every qubit matrix unit evolved through the
+    full column-stacked Liouvillian of each reference segment (exact expm), projected
+    on the qubit block (leakage to |r> is simply lost)."""
+    if p.dim != 3:
+        raise ValueError("process_map: dim 3 only")
+    D = 9
+    props = [sla.expm(liouvillian(H, p.c_ops) * float(t[-1])) for H, t, _ in segments(p)]
+    S = np.zeros((16, 16), dtype=complex)
+    for a in range(4):
+        for b in range(4):
+            rho = np.zeros((D, D), dtype=complex)
+            rho[QUBIT_INDEX[a], QUBIT_INDEX[b]] = 1.0
+            v = vec(rho)
+            for P in props:
+                v = P @ v
+            r = unvec(v, D)
+            for c in range(4):
+                for d in range(4):
+                    S[4 * c + d, 4 * a + b] = r[QUBIT_INDEX[c], QUBIT_INDEX[d]]
+    return S
+
+
+def apply_map(S: np.ndarray, X: np.ndarray) -> np.ndarray:
+    """E(X) for a 4x4 operator X from the matrix-unit map S."""
+    out = np.zeros((4, 4), dtype=complex)
+    for a in range(4):
+        for b in range(4):
+            out += X[a, b] * S[:, 4 * a + b].reshape(4, 4)
+    return out
+
+
+def choi_matrix(S: np.ndarray) -> np.ndarray:
+    """J = sum_ab |a><b| (x) E(|a><b|) (input factor first)."""
+    J = np.zeros((16, 16), dtype=complex)
+    for a in range(4):
+        for b in range(4):
+            Eab = np.zeros((4, 4), dtype=complex)
+            Eab[a, b] = 1.0
+            J += np.kron(Eab, apply_map(S, Eab))
+    return J
+
+
+_PAULI1 = (np.eye(2, dtype=complex), np.array([[0, 1], [1, 0]], dtype=complex),
+           np.array([[0, -1j], [1j, 0]]), np.array([[1, 0], [0, -1]], dtype=complex))
+PAULI2 = [np.kron(P, Q) for P in _PAULI1 for Q in _PAULI1]     # II, IX, ..., ZZ (atom A first)
+
+
+def pauli_transfer_matrix(S: np.ndarray) -> np.ndarray:
+    """R[i, j] = Tr(P_i E(P_j)) / 4."""
+    R = np.zeros((16, 16))
+    for j, Pj in enumerate(PAULI2):
+        EPj = apply_map(S, Pj)
+        for i, Pi in enumerate(PAULI2):
+            R[i, j] = np.real(np.trace(Pi @ EPj)) / 4
+    return R

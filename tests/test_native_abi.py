@@ -29,6 +29,9 @@ def test_header_constants_match_binding():
     for k, v in N.S.items():
         assert int(defs["RYD_S_" + k]) == v
     assert int(defs["RYD_NPARAM"]) == N.NPARAM and int(defs["RYD_NSUMMARY"]) == N.NSUMMARY
+    for k, v in N.C.items():
+        assert int(defs["RYD_C_" + k]) == v
+    assert int(defs["RYD_NCOH"]) == N.NCOH
     for k, v in N.PROTO.items():
         assert int(defs["RYD_PROTO_" + k.upper()]) == v
     assert ctypes.sizeof(N.BatchDesc) == 56 and ctypes.sizeof(N.Stats) == 48
