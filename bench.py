@@ -1,12 +1,15 @@
 """Benchmark: Lindblad parameter points/s on the C2 sweep (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3]
+    python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4]
 
 A step = one propagation of this rank's 10,000-point LP-square (Omega, Delta)
 sweep -- every point's 4 basis density matrices through both pulses, noise
 rates from the reference formulas -- with inputs resident in HBM.  ``--workload
 c3`` runs the 100k-point smooth-JP (Omega, Omega*tau) Pareto sweep instead
-(300 reference segments per point); it is a secondary line, not the metric.  With N > 1
+(300 reference segments per point); ``--workload c4`` the 1M-point species x
+temperature x tweezer-power LP-square grid (BASELINE configs[3]), range-sharded
+over the ranks (strong scaling: the global grid is fixed).  Both are secondary
+lines, not the metric.  With N > 1
 ranks (torch.distributed.run, one process per GPU) the global sweep is N x 10k
 points range-partitioned by Delta/Omega; no collective touches the data path
 (weak scaling); a gloo barrier brackets the timed region and the max time over
@@ -77,13 +80,13 @@ def _max_over_ranks(pg, x: float) -> float:
     return float(t.item())
 
 
-def cpu_baseline(sample: int, procs: int):
+def cpu_baseline(sample: int, procs: int, workload: str = "c2"):
     """QuTiP-like CPU restatement timed on the host cores (oracle/cpu_baseline.py),
     in a clean child process with single-threaded BLAS."""
     import subprocess
     env = dict(os.environ, OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1")
     out = subprocess.run([sys.executable, "-m", "oracle.cpu_baseline", "--sample", str(sample),
-                          "--procs", str(procs)], cwd=REPO, env=env, check=True,
+                          "--procs", str(procs), "--workload", workload], cwd=REPO, env=env, check=True,
                          capture_output=True, text=True, timeout=600)
     return json.loads(out.stdout.strip().splitlines()[-1])
 
@@ -94,10 +97,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=64)
+    ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--method", default="chebyshev",
                     choices=["chebyshev", "cheb_squaring", "cheb_vector"])
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
     args = ap.parse_args()
 
     ws, rank, local, pg = _dist()
@@ -110,11 +113,17 @@ def main():
         protocol, n_steps, n_seg = "lp_square", None, 2
         workload = ("C2: 10k-point (Omega, Delta) LP-square CZ sweep per GPU, medium apparatus, "
                     "full reference noise model (8 Lindblad channels)")
-    else:
+    elif args.workload == "c3":
         batch = SW.c3_rank_shard(rank, ws)
         protocol, n_steps, n_seg = "smooth_jp", 300, 300
         workload = ("C3: 100k-point (Omega, Omega*tau) smooth-JP Pareto sweep per GPU, 300 "
                     "reference segments, medium apparatus, full reference noise model")
+    else:
+        batch = SW.c4_rank_shard(rank, ws)
+        protocol, n_steps, n_seg = "lp_square", None, 2
+        workload = ("C4: 1M-point species {Rb87, Cs133} x T logspace(1-100 uK, 1000) x P_tweezer "
+                    "logspace(1-100 mW, 500) LP-square grid, range-sharded over the ranks, "
+                    "medium apparatus, full reference noise model")
     params = E.pack_params(batch)
     n = batch.n
     eng = E.Engine(devices=[local])
@@ -152,15 +161,17 @@ def main():
     tr = _measured_traffic(args.workload, args.method, n)
     traffic = tr["bytes_per_launch"] if tr else None
 
-    total_points = n * ws * args.steps
+    strong = args.workload == "c4"
+    global_points = SW.C4_POINTS if strong else n * ws
+    total_points = global_points * args.steps
     value = total_points / dt_max
     out = {
         "metric": "Lindblad param-points/sec (2-atom Rydberg CZ sweep); achieved HBM GB/s vs peak",
         "value": value, "unit": "points/s", "n_gpus": ws, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": workload, "points_per_gpu": n, "global_points": n * ws,
+        "config": {"workload": workload, "points_per_gpu": n, "global_points": global_points,
                    "parallelism": f"range-shard x{ws}",
                    "method": args.method + (" (auto: propagator kernel, phase frame)"
                                             if args.method == "chebyshev" else "")},
@@ -175,9 +186,9 @@ def main():
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": bytes_per_point * n},
     }
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.workload == "c2":
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.workload in ("c2", "c4"):
         procs = max(1, min(16, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, procs)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, procs, args.workload)
     if rank == 0:
         print(json.dumps(out), flush=True)
     db.free()

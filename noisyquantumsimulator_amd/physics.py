@@ -189,9 +189,11 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
 
     Any apparatus argument may be an array (broadcast to N).  ``overrides`` may
     hold per-point arrays replacing simulation-input fields
-    (laser_1_power, laser_2_power, laser_1_waist, laser_2_waist, Delta_e,
-    delta_over_omega, omega_tau, A, omega_mod_ratio, phi_offset) -- the batched
-    equivalent of building one simulation_inputs object per point.
+    (laser_1_power, laser_2_power, laser_1_waist, laser_2_waist,
+    laser_1_linewidth_hz, laser_2_linewidth_hz, Delta_e, delta_over_omega,
+    omega_tau, A, omega_mod_ratio, phi_offset; bang-bang switching_times (n, k)
+    and phases (n, k+1)) -- the batched equivalent of building one
+    simulation_inputs object per point.
     """
     from .configurations import (JPSimulationInputs, LPSimulationInputs,
                                  SmoothJPSimulationInputs)
@@ -211,7 +213,8 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
 
     sizes = [np.size(a) for a in (n_rydberg, tweezer_power, tweezer_waist, temperature, B_field,
                                   NA, spacing_factor) if np.ndim(a) > 0]
-    sizes += [np.size(v) for v in ov.values() if np.ndim(v) > 0]
+    sizes += [np.shape(v)[0] for k, v in ov.items() if np.ndim(v) > 0
+              and not (k in ("switching_times", "phases") and np.ndim(v) == 1)]
     if np.ndim(species) > 0:
         sizes.append(np.size(species))
     if tweezer_wavelength_nm is not None and np.ndim(tweezer_wavelength_nm) > 0:
@@ -230,15 +233,17 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
     T, B = _bc(temperature, n), _bc(B_field, n)
     NA_, sf_ = _bc(NA, n), _bc(spacing_factor, n)
 
-    lw1, lw2 = L1.linewidth_hz, L2.linewidth_hz
+    # combined laser linewidth (RG/simulation.py:2854): hypot of the two legs
+    lw1 = ov.get("laser_1_linewidth_hz", L1.linewidth_hz)
+    lw2 = ov.get("laser_2_linewidth_hz", L2.linewidth_hz)
     if lw1 is not None and lw2 is not None:
-        lw = float(np.sqrt(lw1 ** 2 + lw2 ** 2))
+        lw = np.sqrt(_bc(lw1, n) ** 2 + _bc(lw2, n) ** 2)
     elif lw1 is not None:
-        lw = float(lw1)
+        lw = _bc(lw1, n)
     elif lw2 is not None:
-        lw = float(lw2)
+        lw = _bc(lw2, n)
     else:
-        lw = 1000.0
+        lw = np.full(n, 1000.0)
     if Delta_e is None or np.any(np.isnan(Delta_e)):
         raise TypeError("TwoPhotonExcitationConfig.Delta_e must be a number")
 
@@ -393,8 +398,14 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
         cols["tau_total"] = _bc(otv if otv is not None else d["omega_tau"], n) / Om
         cols["tau_single"] = cols["tau_total"].copy()
     elif protocol == "jandura_pupillo":
-        st = ov.get("switching_times", si.switching_times) or list(P.JP_BANGBANG_SWITCHING_TIMES)
-        ph = ov.get("phases", si.phases) or list(P.JP_BANGBANG_PHASES)
+        # `getattr(si, ..., None) or default` (RG/simulation.py:3025-3028): an empty
+        # list falls back to the defaults; per-point (n, k) arrays pass through
+        def _or_default(v, default):
+            if isinstance(v, np.ndarray):
+                return v if v.size else list(default)
+            return v or list(default)
+        st = _or_default(ov.get("switching_times", si.switching_times), P.JP_BANGBANG_SWITCHING_TIMES)
+        ph = _or_default(ov.get("phases", si.phases), P.JP_BANGBANG_PHASES)
         bb_t = np.broadcast_to(np.atleast_2d(np.asarray(st, dtype=float)), (n, np.shape(st)[-1])).copy()
         bb_p = np.broadcast_to(np.atleast_2d(np.asarray(ph, dtype=float)), (n, np.shape(ph)[-1])).copy()
         if bb_p.shape[1] != bb_t.shape[1] + 1:
@@ -410,7 +421,7 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
         cols[k] = np.zeros(n)
     if include_noise:
         cols["gamma_r"] = cols["gamma_r_trap"].copy()
-        cols["gamma_phi_laser"] = np.full(n, np.pi * lw)
+        cols["gamma_phi_laser"] = np.pi * lw
         cols["gamma_loss_background"] = (_bc(background_loss_rate_hz, n)
                                          if background_loss_rate_hz is not None else np.full(n, 1e3))
         g_mot = cols["g_thermal"] if noise.include_motional_dephasing else np.zeros(n)

@@ -82,11 +82,17 @@ def pareto_tgate_grid(n_omega: int = 1000, n_tau: int = 100, include_noise: bool
                            overrides=dict(laser_2_power=p2, omega_tau=OT.ravel()))
 
 
+C4_SHAPE = (2, 1000, 500)          # species x T x P_tweezer
+C4_POINTS = 2 * 1000 * 500
+
+
 def species_temperature_power_grid(n_T: int = 1000, n_P: int = 500, include_noise: bool = True,
-                                   point_slice: Optional[slice] = None) -> PH.DerivedBatch:
+                                   point_slice: Optional[slice] = None,
+                                   point_index: Optional[np.ndarray] = None) -> PH.DerivedBatch:
     """C4: species {Rb87, Cs133} x T in logspace(1, 100) uK x P_tweezer in logspace(1, 100) mW,
-    LP square, medium apparatus otherwise.  ``point_slice`` selects a contiguous range
-    shard (multi-GPU range partition) before derivation."""
+    LP square, medium apparatus otherwise.  Point order is
+    species-major, then T, then P.  ``point_slice`` (a contiguous range shard, the
+    multi-GPU partition) or ``point_index`` selects points before derivation."""
     warnings.simplefilter("ignore")
     sp = np.array(["Rb87", "Cs133"])
     T = np.logspace(-6, -4, n_T)
@@ -95,9 +101,25 @@ def species_temperature_power_grid(n_T: int = 1000, n_P: int = 500, include_nois
     S_, T_, P_ = S_.ravel(), T_.ravel(), P_.ravel()
     if point_slice is not None:
         S_, T_, P_ = S_[point_slice], T_[point_slice], P_[point_slice]
+    if point_index is not None:
+        S_, T_, P_ = S_[point_index], T_[point_index], P_[point_index]
     return PH.derive_batch(CF.LPSimulationInputs(excitation=medium_excitation()), n=T_.size,
                            **_apparatus_kwargs(species=sp[S_], temperature=T_, tweezer_power=P_),
                            include_noise=include_noise)
+
+
+def range_shard(n: int, rank: int, world_size: int) -> slice:
+    """Contiguous range partition: point i -> rank floor(world_size * i / n)."""
+    if not 0 <= rank < world_size:
+        raise ValueError("rank out of range")
+    return slice(n * rank // world_size, n * (rank + 1) // world_size)
+
+
+def c4_rank_shard(rank: int, world_size: int, include_noise: bool = True) -> PH.DerivedBatch:
+    """Strong-scaling shard of the fixed 1M-point C4 grid: rank r owns the contiguous
+    range [r N / W, (r+1) N / W) -- no data exchange between ranks."""
+    return species_temperature_power_grid(include_noise=include_noise,
+                                          point_slice=range_shard(C4_POINTS, rank, world_size))
 
 
 def c2_rank_shard(rank: int, world_size: int, points_per_rank_delta: int = 100,

@@ -2,7 +2,7 @@
 
 Times the QuTiP-like oracle (ZVODE Adams at the reference tolerances, the
 reference's tlists and per-segment restarts; oracle/lindblad_oracle.py) on a
-bounded sample of the C2 sweep, in a fresh process with single-threaded BLAS
+bounded sample of the C2 (or C4) sweep, in a fresh process with single-threaded BLAS
 and a fork pool of worker processes.
 
     OPENBLAS_NUM_THREADS=1 python -m oracle.cpu_baseline --sample 96 --procs 16
@@ -35,11 +35,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sample", type=int, default=96)
     ap.add_argument("--procs", type=int, default=8)
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4"])
     a = ap.parse_args()
     from noisyquantumsimulator_amd import sweeps as SW
-    b = SW.omega_delta_grid()
+    if a.workload == "c2":
+        b = SW.omega_delta_grid()
+        idx = np.linspace(0, b.n - 1, a.sample).astype(int)
+        what = "the C2 10k sweep"
+    else:   # derive only the sampled points of the 1M grid
+        full = np.linspace(0, SW.C4_POINTS - 1, a.sample).astype(int)
+        b = SW.species_temperature_power_grid(point_index=full)
+        idx = np.arange(a.sample)
+        what = "the C4 1M grid"
     c = b.cols
-    idx = np.linspace(0, b.n - 1, a.sample).astype(int)
     specs = [O.PointSpec(protocol="lp_square", Omega=c["Omega"][i], V=c["V"][i],
                          Delta=c["Delta_gate"][i], tau=c["tau_single"][i],
                          xi=complex(c["xi_re"][i], c["xi_im"][i]),
@@ -52,7 +60,7 @@ def main():
     wall = time.perf_counter() - t0
     print(json.dumps(dict(
         value=a.sample / wall, unit="points/s", cores=a.procs, kind="port",
-        sample=f"{a.sample} points evenly spaced over the C2 10k sweep; oracle ZVODE-Adams "
+        sample=f"{a.sample} points evenly spaced over {what}; oracle ZVODE-Adams "
                f"restatement of qutip.mesolve (atol 1e-10, rtol 1e-8, reference tlists); "
                f"{a.procs} single-threaded worker processes; {wall:.2f} s wall")))
 
