@@ -150,6 +150,7 @@ class DerivedBatch:
     bangbang_times: Optional[np.ndarray] = None     # (n, nseg-1) dimensionless
     bangbang_phases: Optional[np.ndarray] = None    # (n, nseg)
     warnings: list = field(default_factory=list)
+    noise_config: Any = None                        # the NoiseSourceConfig the points share
 
     def __getitem__(self, k):
         return self.cols[k]
@@ -448,7 +449,8 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
             cols["combined_polarization_purity"] = np.full(n, pur)
     return DerivedBatch(protocol=protocol, pulse_shape=pulse_shape, dim=hilbert_space_dim,
                         include_noise=include_noise, trap_laser_on=trap_laser_on, n=n, cols=cols,
-                        bangbang_times=bb_t, bangbang_phases=bb_p, warnings=flags)
+                        bangbang_times=bb_t, bangbang_phases=bb_p, warnings=flags,
+                        noise_config=noise)
 
 
 def area_correction_factor(pulse_shape: str, tau) -> np.ndarray:

@@ -340,6 +340,36 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                        is_mixed=~ket_mask, states=out_states, kernel_ms=kms)
 
 
+def noise_breakdown_row(b: PH.DerivedBatch, i: int, n_collapse_ops: Optional[int] = None) -> Dict[str, Any]:
+    """SimulationResult.noise_breakdown of point i of a derived batch
+    (RG/simulation.py:3230-3334 and the dict it returns)."""
+    c = {k: (v[i] if np.ndim(v) > 0 else v) for k, v in b.cols.items()}
+    motional = b.noise_config.include_motional_dephasing if b.noise_config is not None else True
+    nb = {"total_decay_rate": 0.0, "total_dephasing_rate": 0.0, "total_loss_rate": 0.0,
+          "n_collapse_ops": 0, "motional_dephasing_included": motional,
+          "gamma_scatter_intermediate": c["g_scatter"], "Omega1_MHz": c["Omega1"] / (2 * np.pi * 1e6)}
+    if not b.include_noise:
+        return nb
+    rates = {k: c[k] for k in PH.RATE_FIELDS}
+    if n_collapse_ops is None:
+        n_collapse_ops = len(OPS.collapse_operators(rates, b.dim))
+    gphi = rates["gamma_phi_laser"] + rates["gamma_phi_thermal"] + rates["gamma_phi_zeeman"]
+    nb.update(rates)
+    nb.update(
+        branching_1=0.5, gamma_phi_total=gphi, total_decay_rate=rates["gamma_r"] + rates["gamma_bbr"],
+        total_dephasing_rate=gphi,
+        total_loss_rate=rates["gamma_loss_antitrap"] + rates["gamma_loss_background"] + rates["gamma_leakage"],
+        dim=b.dim, n_collapse_ops=n_collapse_ops,
+        gamma_blockade_fluct=c["g_thermal"] if motional else 0.0,
+        gamma_doppler=c["g_doppler"], gamma_intensity_noise=c["g_intensity"],
+        gamma_thermal_total=rates["gamma_phi_thermal"],
+        delta_V_over_V_percent=c["dVV"] * 100, anti_trap_time_factor=c.get("anti_trap_time_factor", 0.0),
+        magic_enhancement=c["enhancement"], alpha_ratio=c["alpha_ratio"],
+        k_eff_rad_per_m=c["k_eff"], v_thermal_m_per_s=c["v_thermal"],
+        gamma_mJ_leakage=rates["mJ_leakage_rate"])
+    return nb
+
+
 def _protocol_name(protocol: str) -> str:
     return {"levine_pichler": "levine_pichler", "smooth_jp": "smooth_jp",
             "jandura_pupillo": "jandura_pupillo"}[protocol]
@@ -386,27 +416,7 @@ def simulate_CZ_gate(
         H2 = OPS.hamiltonian(c["Omega"] * xi, c["Delta_gate"], c["V"], 3, d1)
     rates = {k: c[k] for k in PH.RATE_FIELDS}
     c_ops = OPS.collapse_operators(rates, hilbert_space_dim) if include_noise else []
-    si = simulation_inputs
-    noise_breakdown = {
-        "total_decay_rate": 0.0, "total_dephasing_rate": 0.0, "total_loss_rate": 0.0,
-        "n_collapse_ops": 0, "motional_dephasing_included": si.noise.include_motional_dephasing,
-        "gamma_scatter_intermediate": c["g_scatter"], "Omega1_MHz": c["Omega1"] / (2 * np.pi * 1e6),
-    }
-    if include_noise:
-        gphi = rates["gamma_phi_laser"] + rates["gamma_phi_thermal"] + rates["gamma_phi_zeeman"]
-        noise_breakdown.update(rates)
-        noise_breakdown.update(
-            branching_1=0.5, gamma_phi_total=gphi, total_decay_rate=rates["gamma_r"] + rates["gamma_bbr"],
-            total_dephasing_rate=gphi,
-            total_loss_rate=rates["gamma_loss_antitrap"] + rates["gamma_loss_background"] + rates["gamma_leakage"],
-            dim=hilbert_space_dim, n_collapse_ops=len(c_ops),
-            gamma_blockade_fluct=c["g_thermal"] if si.noise.include_motional_dephasing else 0.0,
-            gamma_doppler=c["g_doppler"], gamma_intensity_noise=c["g_intensity"],
-            gamma_thermal_total=rates["gamma_phi_thermal"],
-            delta_V_over_V_percent=c["dVV"] * 100, anti_trap_time_factor=c.get("anti_trap_time_factor", 0.0),
-            magic_enhancement=c["enhancement"], alpha_ratio=c["alpha_ratio"],
-            k_eff_rad_per_m=c["k_eff"], v_thermal_m_per_s=c["v_thermal"],
-            gamma_mJ_leakage=rates["mJ_leakage_rate"])
+    noise_breakdown = noise_breakdown_row(b, 0, len(c_ops))
     A0 = 0.529e-10
     from .constants import EPS0
     au = 4 * np.pi * EPS0 * A0 ** 3
@@ -441,7 +451,7 @@ def simulate_CZ_gate(
         omega_r_kHz=c["omega_r"] / (2 * np.pi * 1e3), sigma_r_nm=c["sigma_r"] * 1e9,
         trap_wavelength_nm=c["wavelength_nm"], magic_wavelength_analysis=magic,
         noise_breakdown=noise_breakdown, include_noise=include_noise,
-        include_motional_dephasing=si.noise.include_motional_dephasing, pulse_info=pulse_info,
+        include_motional_dephasing=simulation_inputs.noise.include_motional_dephasing, pulse_info=pulse_info,
         config=config, species=config.species, n_rydberg=config.n_rydberg, qubit_0=config.qubit_0,
         qubit_1=config.qubit_1, temperature_K=temperature, B_field_T=B_field,
         delta_zeeman=c["delta_zeeman"], delta_stark=c["delta_stark"] if trap_laser_on else 0.0,

@@ -1,0 +1,54 @@
+"""CPU batched-metrics evaluator built on the oracle -- TEST INFRASTRUCTURE ONLY.
+
+Same signature as noisyquantumsimulator_amd.optimize_cz_gate.default_batch_evaluator
+(the GPU engine), so the optimiser drivers can be exercised on CPU: host
+derivation (the product's vectorised a1), then per point the expm oracle
+(oracle/lindblad_oracle.py) and its compute_CZ_fidelity restatement.
+"""
+import warnings
+
+import numpy as np
+
+from noisyquantumsimulator_amd import physics as PH
+from oracle import lindblad_oracle as O
+
+CALLS = []          # batch sizes seen, for tests that count engine passes
+
+
+def point_spec(b, i, n_steps=300):
+    c = b.cols
+    kw = dict(Omega=c["Omega"][i], V=c["V"][i], delta_zeeman=c["delta_zeeman"][i],
+              delta_stark=c["delta_stark"][i], trap_laser_on=b.trap_laser_on,
+              c_ops=O.collapse_operators({k: c[k][i] for k in O.RATE_KEYS}) if b.include_noise else [])
+    if b.protocol == "levine_pichler":
+        return O.PointSpec(protocol="lp_square", Delta=c["Delta_gate"][i], tau=c["tau_single"][i],
+                           xi=complex(c["xi_re"][i], c["xi_im"][i]), **kw)
+    if b.protocol == "smooth_jp":
+        return O.PointSpec(protocol="smooth_jp", Delta=c["Delta_seg"][i], tau=c["tau_total"][i], A=c["A"][i],
+                           omega_mod=c["omega_mod"][i], phi_offset=c["phi_offset"][i], n_steps=n_steps, **kw)
+    return O.PointSpec(protocol="bangbang", omega_tau=c["omega_tau"][i],
+                       switching_times=list(b.bangbang_times[i]), phases=list(b.bangbang_phases[i]), **kw)
+
+
+def oracle_batch_evaluator(simulation_inputs, n, include_noise, overrides, **apparatus):
+    CALLS.append(n)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        b = PH.derive_batch(simulation_inputs, n, include_noise=include_noise, overrides=overrides,
+                            **apparatus)
+    keys = ("controlled_phase_deg", "phase_error_deg", "cz_phase_fidelity", "f00", "f01", "f10", "f11",
+            "avg_fidelity", "gate_time_us", "V_over_Omega", "Omega_MHz")
+    m = {k: np.zeros(b.n) for k in keys}
+    for i in range(b.n):
+        fid, avg, info = O.cz_fidelity(O.run_point(point_spec(b, i)))
+        m["controlled_phase_deg"][i] = info["controlled_phase_deg"]
+        m["phase_error_deg"][i] = info["phase_error_from_pi_deg"]
+        m["cz_phase_fidelity"][i] = info["cz_phase_fidelity"]
+        for lab in ("00", "01", "10", "11"):
+            m["f" + lab][i] = fid[lab]
+        m["avg_fidelity"][i] = avg
+    m["gate_time_us"] = b.cols["tau_total"] * 1e6
+    m["V_over_Omega"] = b.cols["V_over_Omega"].copy()
+    m["Omega_MHz"] = b.cols["Omega"] / (2 * np.pi * 1e6)
+    m["_batch"] = b
+    return m, np.ones(b.n, bool)

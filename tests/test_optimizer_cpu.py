@@ -1,0 +1,236 @@
+"""Batched optimiser drivers on CPU, with the oracle as the
+batched evaluator (tests/oracle_evaluator.py).  The GPU form of the same drivers
+is exercised in tests/test_gpu_optimizer.py."""
+import hashlib
+import warnings
+
+import numpy as np
+import pytest
+from scipy.optimize import differential_evolution
+
+import oracle_evaluator as OE
+from noisyquantumsimulator_amd import configurations as CF
+from noisyquantumsimulator_amd import optimize_cz_gate as OC
+from noisyquantumsimulator_amd import physics as PH
+
+
+def test_compute_cost_matches_reference_formula():
+    m = dict(avg_fidelity=0.99, f11=0.97, cz_phase_fidelity=0.98)
+    want = 10 * 1.0 ** 2 + 5 * 3.0 ** 2 + 2 * 2.0 ** 2 + 0.01 * 0.4
+    assert OC.compute_cost(m, gate_time_us=0.4) == pytest.approx(want, rel=1e-12)
+    assert OC.compute_cost(dict(avg_fidelity=0.49, f11=1, cz_phase_fidelity=1)) == 1e6
+    assert OC.compute_cost(dict(avg_fidelity=np.nan, f11=1, cz_phase_fidelity=1)) == 1e6
+    c = OC.compute_cost_batch({"avg_fidelity": np.array([0.99, 0.3]), "f11": np.array([0.97, 1.0]),
+                               "cz_phase_fidelity": np.array([0.98, 1.0])}, np.array([0.4, 0.1]))
+    assert c[0] == pytest.approx(want) and c[1] == 1e6
+
+
+def test_cache_keys_and_persistence(tmp_path):
+    c = OC.SimulationCache(precision=4)
+    k = c.make_key("smooth_jp", [10.09123456, 0.311], "abc")
+    assert k == "abc|smooth_jp|(10.0912, 0.311)"
+    c[k] = (1.5, {"avg_fidelity": 0.9})
+    assert k in c and len(c) == 1
+    p = tmp_path / "cache.json"
+    c.save(str(p))
+    d = OC.SimulationCache()
+    d.load(str(p))
+    assert d[k] == (1.5, {"avg_fidelity": 0.9}) and d.hits == 1
+
+
+def test_apparatus_fingerprint():
+    a = OC.ApparatusConstraints()
+    vals = (round(50e-6, 8), round(50e-6, 8), round(0.3, 8), round(50e-6, 8), round(2 * np.pi * 1e9, 2), 70,
+            round(2.8, 4), round(2e-6, 10), "Rb87", round(0.020, 6), round(0.8e-6, 8), round(0.5, 3))
+    assert a.fingerprint() == hashlib.md5(str(vals).encode()).hexdigest()[:12]
+    assert OC.ApparatusConstraints(temperature=3e-6).fingerprint() != a.fingerprint()
+    exc = a.make_excitation_config(0.99)
+    assert exc.laser_1.polarization == "pi" and exc.laser_2.polarization == "sigma+"
+    assert exc.laser_1.polarization_purity == 0.99
+
+
+def test_bangbang_population_overrides_match_per_point_inputs():
+    """The batched bang-bang parameterisation (fractions -> sorted times) derives
+    exactly what the reference builds per candidate with _build_jp_bangbang_inputs."""
+    warnings.simplefilter("ignore")
+    rng = np.random.default_rng(3)
+    space = OC._param_space("jp_bangbang", 5)
+    lo, hi = np.array(space.bounds).T
+    X = lo + (hi - lo) * rng.random((6, len(lo)))
+    a = OC.ApparatusConstraints()
+    exc, noise = a.make_excitation_config(1.0), a.make_noiseless()
+    si, over = space.inputs(X, exc, noise)
+    b = PH.derive_batch(si, X.shape[0], include_noise=False, overrides=over, **a.simulate_kwargs())
+    for i in range(X.shape[0]):
+        si1 = OC._build_jp_bangbang_inputs(X[i], exc, noise, n_segments=5)
+        b1 = PH.derive_batch(si1, include_noise=False, **a.simulate_kwargs())
+        np.testing.assert_array_equal(b.bangbang_times[i], b1.bangbang_times[0])
+        np.testing.assert_array_equal(b.bangbang_phases[i], b1.bangbang_phases[0])
+        assert b["tau_total"][i] == b1["tau_total"][0]
+    assert np.all(np.diff(b.bangbang_times, axis=1) >= 0)
+
+
+def test_smooth_jp_and_lp_population_overrides():
+    warnings.simplefilter("ignore")
+    a = OC.ApparatusConstraints()
+    exc, noise = a.make_excitation_config(1.0), a.make_noiseless()
+    for proto, build in (("smooth_jp", OC._build_smooth_jp_inputs), ("lp", OC._build_lp_inputs)):
+        space = OC._param_space(proto)
+        X = np.array([space.x0, np.array(space.bounds).mean(axis=1)])
+        si, over = space.inputs(X, exc, noise)
+        b = PH.derive_batch(si, 2, include_noise=False, overrides=over, **a.simulate_kwargs())
+        for i in range(2):
+            b1 = PH.derive_batch(build(X[i], exc, noise), include_noise=False, **a.simulate_kwargs())
+            for k in ("tau_total", "Delta_seg", "omega_tau", "xi_re", "xi_im"):
+                assert b[k][i] == b1[k][0], (proto, k)
+
+
+def test_per_point_linewidth_override():
+    warnings.simplefilter("ignore")
+    si = CF.LPSimulationInputs()
+    lw = np.array([100.0, 5e3])
+    b = PH.derive_batch(si, 2, overrides=dict(laser_1_linewidth_hz=lw, laser_2_linewidth_hz=lw))
+    np.testing.assert_allclose(b["gamma_phi_laser"], np.pi * np.sqrt(2) * lw, rtol=1e-15)
+
+
+def test_warm_start_bounds():
+    r = OC.OptimizationResult(success=True, protocol="jp_bangbang", best_params=np.array([20.0, 0.5, 0.1]),
+                              param_names=["omega_tau", "frac1", "phi0"], best_cost=0.0, best_metrics={},
+                              n_evaluations=0, runtime_s=0.0)
+    b, x0 = OC.warm_start_bounds(r, 0.2, [(5.0, 22.0), (0.01, 0.99), (-np.pi, np.pi)])
+    assert b[0] == (16.0, 22.0)
+    assert b[1] == pytest.approx((0.3, 0.7))
+    assert b[2] == pytest.approx((0.1 - 0.2 * np.pi, 0.1 + 0.2 * np.pi))
+    np.testing.assert_array_equal(x0, r.best_params)
+
+
+def _objective(cache=None):
+    a = OC.ApparatusConstraints()
+    space = OC._param_space("lp")
+    return OC._Objective(space, a.make_excitation_config(1.0), a.make_noiseless(), a, False, 0.01,
+                         cache or OC.SimulationCache(), False, OE.oracle_batch_evaluator, False), space
+
+
+def test_vectorized_de_follows_the_deferred_trajectory():
+    """One batched evaluation per generation reproduces scipy's deferred-updating DE
+    run with a per-candidate objective exactly (same seed, same trial vectors)."""
+    ov, space = _objective()
+    os_, _ = _objective()
+    kw = dict(bounds=space.bounds, x0=space.x0, maxiter=2, popsize=3, tol=1e-6, seed=42, polish=False,
+              updating="deferred")
+    OE.CALLS.clear()
+    rv = differential_evolution(ov.vec, vectorized=True, **kw)
+    n_vec_calls = len(OE.CALLS)
+    rs = differential_evolution(os_.scalar, **kw)
+    np.testing.assert_array_equal(rv.x, rs.x)
+    assert rv.fun == rs.fun
+    assert n_vec_calls <= 3 and ov.n_batches == n_vec_calls     # init + 2 generations
+    assert os_.n_batches > 3 * n_vec_calls
+
+
+def test_optimize_cz_gate_lp_on_oracle():
+    a = OC.ApparatusConstraints()
+    cache = OC.SimulationCache()
+    OE.CALLS.clear()
+    r = OC.optimize_cz_gate("lp", a, include_noise=False, maxiter=2, popsize=3, cache=cache, verbose=False,
+                            evaluator=OE.oracle_batch_evaluator)
+    assert r.protocol == "lp" and r.param_names == ["delta_over_omega", "omega_tau"]
+    assert r.discrete_variant == "default"
+    base = OC.run_baseline("lp", a, include_noise=False, verbose=False, evaluator=OE.oracle_batch_evaluator)
+    # x0 = the asymptotic LP point is in the initial population: DE can only improve on it
+    x0_cost = cache[cache.make_key("lp", list(OC._get_lp_bounds_and_x0()[1]),
+                                   f"{a.fingerprint()}_n{OC._noise_hash(a.make_noiseless())}")][0]
+    assert r.best_cost <= x0_cost + 1e-12
+    assert r.best_metrics["avg_fidelity"] > 0.99 and base["avg_fidelity"] > 0.99
+    assert r.n_evaluations >= 6 and r.n_batches < r.n_evaluations
+    assert max(OE.CALLS) == 6                    # whole population in one evaluator call
+    # second run: every DE member is a cache hit (same seed -> same candidates)
+    r2 = OC.optimize_cz_gate("lp", a, include_noise=False, maxiter=2, popsize=3, cache=cache, verbose=False,
+                             evaluator=OE.oracle_batch_evaluator)
+    assert r2.cache_hits >= 6 and r2.best_cost == r.best_cost
+
+
+def test_unknown_protocol_and_variant():
+    a = OC.ApparatusConstraints()
+    with pytest.raises(ValueError):
+        OC.optimize_cz_gate("foo", a, verbose=False)
+    with pytest.raises(ValueError):
+        OC.optimize_cz_gate("jp_bangbang", a, variant="6-segment", verbose=False)
+    with pytest.raises(ValueError):
+        OC._get_jp_bangbang_bounds_and_x0(6)
+
+
+# ---------------------------------------------------------------------------
+# inverse problem / exploration (noisyquantumsimulator_amd.optimization)
+# ---------------------------------------------------------------------------
+
+from noisyquantumsimulator_amd import optimization as OPT  # noqa: E402
+
+
+def test_pareto_front_and_queries():
+    r = OPT.ExplorationResult(protocol="lp", species="Rb87")
+    for F, t in ((0.9, 100), (0.95, 200), (0.93, 150), (0.99, 400), (0.98, 300)):
+        r.add_point(OPT.EvaluatedPoint(Omega_MHz=1, laser_linewidth_kHz=1, V_over_Omega=100, fidelity=F,
+                                       gate_time_ns=t, infidelity=1 - F))
+    r.compute_pareto_front()
+    assert [(p.fidelity, p.gate_time_ns) for p in r.pareto_front] == [(0.9, 100), (0.93, 150), (0.95, 200),
+                                                                      (0.98, 300), (0.99, 400)]
+    assert r.get_best_for_target(target_fidelity=0.97).gate_time_ns == 300
+    assert r.get_best_for_target(target_time_ns=250).fidelity == 0.95
+    assert r.get_best_for_target(target_fidelity=0.999) is None
+    c = OPT.combine_explorations(r, r)
+    assert c.n_evaluations == 10 and len(c.pareto_front) >= 5
+    assert "Pareto front" in r.summary()
+
+
+def test_exploration_json_roundtrip(tmp_path):
+    r = OPT.ExplorationResult(protocol="lp", species="Rb87")
+    r.add_point(OPT.EvaluatedPoint(Omega_MHz=2.0, laser_linewidth_kHz=0.1, V_over_Omega=50.0, fidelity=0.9,
+                                   gate_time_ns=300.0, infidelity=0.1, noise_breakdown={"gamma_r": 7000.0}))
+    r.compute_pareto_front()
+    p = tmp_path / "x.json"
+    r.save(str(p))
+    q = OPT.ExplorationResult.load(str(p))
+    assert q.points == r.points and q.pareto_front == r.pareto_front
+
+
+def _analytic_evaluator(simulation_inputs, n, include_noise, overrides, **apparatus):
+    """Host derivation + a smooth stand-in fidelity (the DE plumbing under test does
+    not depend on the physics; the expm oracle with L-BFGS polish takes minutes)."""
+    OE.CALLS.append(n)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        b = PH.derive_batch(simulation_inputs, n, include_noise=include_noise, overrides=overrides, **apparatus)
+    c = b.cols
+    F = 1.0 - 1e-6 * (c["tau_total"] * 1e9) * (1 + np.sum([c[k] for k in PH.RATE_FIELDS], axis=0) / 1e6) \
+        - 0.1 / np.maximum(c["V_over_Omega"], 1.0)
+    m = {k: np.full(b.n, np.nan) for k in OC.METRIC_KEYS}
+    m.update(avg_fidelity=F, gate_time_us=c["tau_total"] * 1e6, V_over_Omega=c["V_over_Omega"],
+             Omega_MHz=c["Omega"] / (2 * np.pi * 1e6), _batch=b)
+    return m, np.ones(b.n, bool)
+
+
+def test_explore_parameter_space_records_every_evaluation():
+    OE.CALLS.clear()
+    r = OPT.explore_parameter_space("levine_pichler", maxiter=1, popsize=1, verbose=False,
+                                    evaluator=_analytic_evaluator)
+    # each generation is ONE evaluator call over the population (10 dims x popsize 1)
+    assert OE.CALLS[0] == 10 and OE.CALLS[1] == 10
+    assert r.n_evaluations == sum(OE.CALLS) == len(r.points)
+    assert r.pareto_front and all(0 < p.fidelity <= 1 for p in r.points)
+    assert all("gamma_r" in p.noise_breakdown for p in r.points)
+
+
+def test_optimize_cz_parameters_batched_and_scalar():
+    kw = dict(target_fidelity=0.99, target_gate_time_ns=400, maxiter=1, popsize=1, polish=False, verbose=False,
+              evaluator=OE.oracle_batch_evaluator, include_noise=False,
+              fixed_params=dict(n_rydberg=70, tweezer_power=20e-3, tweezer_waist=1e-6, laser_linewidth=100.0,
+                                temperature=2e-6, Delta_e=1e9, spacing_factor=3.0))
+    rv = OPT.optimize_CZ_parameters(**kw)
+    rs = OPT.optimize_CZ_parameters(vectorized=False, **kw)
+    for r in (rv, rs):
+        assert 0.5 < r.achieved_fidelity <= 1 and r.achieved_gate_time_ns > 0
+        assert set(r.optimal_parameters) >= {"rydberg_power_2", "rydberg_power_1", "delta_over_omega",
+                                             "omega_tau", "laser_linewidth", "n_rydberg"}
+        assert isinstance(r.optimal_parameters["n_rydberg"], int)
+    assert rv.n_evaluations == rs.n_evaluations
