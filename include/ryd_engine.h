@@ -30,6 +30,10 @@
  * every other element of rho is structurally zero, as in QuTiP.  The host
  * expands it to the QuTiP column-stacked 9x9 rho (noisyquantumsimulator_amd.engine).
  * Ket state rows: 9 complex amplitudes, interleaved (re, im), basis 3*a1 + a2.
+ * dim 4 (mJ sublevels): Lindblad rows are the 36 coordinates R[i][j] over
+ * e = {|0><0|, |1><1|, |r+><r+|, |1><r+|+h.c., i(|1><r+|-h.c.), |r-><r-|} (the sigma+
+ * drive never couples |r->, and no jump creates an |r-> coherence, so this is again
+ * the exact invariant sector); ket rows are 16 complex amplitudes, basis 4*a1 + a2.
  *
  * Ownership/threading: the caller owns every buffer; the library never keeps a
  * pointer after return (device-buffer calls: until the stream work completes).
@@ -48,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RYD_ABI_VERSION 1
+#define RYD_ABI_VERSION 2
 
 /* ---- return codes ---- */
 #define RYD_OK              0
@@ -108,7 +112,9 @@ extern "C" {
 #define RYD_P_NSEG       20  /* bang-bang number of segments (<= 8)                       */
 #define RYD_P_SWT0       21  /* bang-bang dimensionless switching times [7]               */
 #define RYD_P_PHI0       28  /* bang-bang segment phases [8]                              */
-#define RYD_NPARAM       36
+#define RYD_P_GMJ_A      36  /* dim 4: atom A mJ mixing |r-><r+| and |r+><r-| rate        */
+#define RYD_P_GMJ_B      37
+#define RYD_NPARAM       38
 
 /* ---- per-point summary columns ---- */
 #define RYD_S_POP0       0   /* <x|rho_x|x> (or |<x|psi_x>|^2), x = 00,01,10,11 (4 cols) */
@@ -151,7 +157,9 @@ extern "C" {
 
 typedef struct ryd_batch_desc {
     int32_t abi_version;     /* = RYD_ABI_VERSION */
-    int32_t dim;             /* single-atom levels: 3 */
+    int32_t dim;             /* single-atom levels: 3, or 4 (|0>,|1>,|r+>,|r->; sigma+ drive,
+                                RG/hamiltonians.py:490-516, :655-679, :741-753, :835-853;
+                                methods CHEBYSHEV / CHEB_VECTOR only) */
     int32_t protocol;        /* RYD_PROTO_* */
     int32_t evolution;       /* RYD_EVOL_* */
     int32_t method;          /* RYD_METHOD_* */

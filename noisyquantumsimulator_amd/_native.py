@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RYD_ENGINE_LIB") or os.path.join(_HERE, "libryd_engine.so")
 
 # keep in sync with include/ryd_engine.h
-RYD_ABI_VERSION = 1
+RYD_ABI_VERSION = 2
 RYD_OK = 0
 PROTO = {"lp_square": 0, "lp_shaped": 1, "bangbang": 2, "smooth_jp": 3}
 EVOL = {"lindblad": 0, "ket": 1}
@@ -24,13 +24,14 @@ FLAG_SYMMETRIC_ATOMS = 1
 
 P = dict(OMEGA=0, DELTA=1, V=2, DELTA1=3, G1_A=4, G0_A=5, GPHI_A=6, GSC_A=7, G1_B=8, G0_B=9,
          GPHI_B=10, GSC_B=11, TAU=12, XI_RE=13, XI_IM=14, AREA_CORR=15, A=16, OMEGA_MOD=17,
-         PHI_OFF=18, OMEGA_TAU=19, NSEG=20, SWT0=21, PHI0=28)
-NPARAM = 36
+         PHI_OFF=18, OMEGA_TAU=19, NSEG=20, SWT0=21, PHI0=28, GMJ_A=36, GMJ_B=37)
+NPARAM = 38
 S = dict(POP0=0, OV_RE0=4, OV_IM0=8, AVG_POP=12, CTRL_PHASE=13, PENALTY=14, AVG_F=15,
          NMV_USEFUL=16, NMV_EXEC=17, TRACE11=18, NSQUARE=19)
 NSUMMARY = 20
 STATUS_NONFINITE, STATUS_STEP_CAP, STATUS_BAD_INPUT = 1, 2, 4
-STATE_WIDTH = {"lindblad": 25, "ket": 18}
+STATE_WIDTH = {"lindblad": 25, "ket": 18}                 # dim 3
+STATE_WIDTH_DIM = {3: STATE_WIDTH, 4: {"lindblad": 36, "ket": 32}}
 # process-map coherence rows (ryd_run_coherences)
 C = dict(K0=0, K1=8, K2=16, K3=18)
 NCOH = 20

@@ -502,7 +502,7 @@ __global__ __launch_bounds__(BLOCK) void lindblad_cheb_kernel(
   }
 }
 
-template <int PROTO>
+template <int PROTO, int KD>
 __global__ __launch_bounds__(BLOCK) void ket_cheb_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ st, int64_t lds,
     double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
@@ -556,8 +556,19 @@ __global__ __launch_bounds__(BLOCK) void ket_cheb_kernel(
   if (over_cap) stat |= RYD_STATUS_STEP_CAP;
   if (!finite_all(v, 18)) stat |= RYD_STATUS_NONFINITE;
   if (live) {
+    if (KD == 3) {
 #pragma unroll
-    for (int e = 0; e < 18; ++e) st[(int64_t)e * lds + gid] = v[e];
+      for (int e = 0; e < 18; ++e) st[(int64_t)e * lds + gid] = v[e];
+    } else {   // dim 4: the sigma+ drive never populates |r->, whose amplitudes stay 0
+#pragma unroll
+      for (int s4 = 0; s4 < 16; ++s4) {
+        const int b1 = s4 >> 2, b2 = s4 & 3;
+        const bool in3 = b1 < 3 && b2 < 3;
+        const int s3 = in3 ? 3 * b1 + b2 : 0;
+        st[(int64_t)(2 * s4) * lds + gid] = in3 ? v[2 * s3] : 0.0;
+        st[(int64_t)(2 * s4 + 1) * lds + gid] = in3 ? v[2 * s3 + 1] : 0.0;
+      }
+    }
   }
   const int lane = threadIdx.x & 63, base = lane & ~3;
   double orr[4], oii[4];
@@ -603,6 +614,167 @@ __global__ __launch_bounds__(BLOCK) void ket_cheb_kernel(
     sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = 4.0 * nuse;
     sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = 4.0 * nexec;
     sm[(int64_t)RYD_S_TRACE11 * ldm + i] = nrm11;
+    sm[(int64_t)RYD_S_NSQUARE * ldm + i] = 0.0;
+    status[i] = st_all;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dim 4 (mJ sublevels |r+>, |r->) Lindblad kernel on the 36-dim real sector
+// ---------------------------------------------------------------------------
+// RG/hamiltonians.py:655-663 (sigma+ drives |1> <-> |r+> only), :741-753 (-Delta on
+// both r+-, zeeman_splitting 0), :835-853 (V on every r(+-) r(+-) pair);
+// RG/noise_models.py:1253-1295 (decay and losses from both r+-, mJ mixing
+// |r-><r+| and |r+><r-| at the same rate gm, dephasing on P_r+ and P_r-), :1415
+// (scattering on P_1).  No |r-> coherence is ever created, so the basis inputs
+// live in span{e00, e11, e++, ex, ey, e--} per atom.  Single-atom generator rows
+// (output) over columns (input):
+//   e00: [0, 0,   g0,        0,    0,   g0       ]
+//   e11: [0, 0,   g1,        2hy, -2hx, g1       ]
+//   e++: [0, 0, -(g0+g1+gm), -2hy, 2hx, gm       ]
+//   ex : [0, -hy, hy,       -G,   2hz,  0        ]
+//   ey : [0,  hx, -hx,      -2hz, -G,   0        ]
+//   e--: [0, 0,   gm,        0,    0, -(g0+g1+gm)]
+// G = (g1+g0+gphi+gsc+gm)/2; V P_R (x) P_R with P_R = P_r+ + P_r- gives (V/2)(S (x) D +
+// D (x) S), S: e++, e-- -> 2x, ex, ey -> 1x; D: ex -> ey, ey -> -ex.
+struct Gen4 {
+  double g0, g1, gm, mg, hx, hy, hx2, hy2, hz2, G;
+};
+
+__device__ __forceinline__ Gen4 make_gen4(const Seg& g, double d1, const double* r, double gm, double s) {
+  Gen4 a;
+  const double hx = 0.5 * g.om_re, hy = -0.5 * g.om_im, hz = 0.5 * (d1 + g.dl);
+  a.g0 = s * r[1];
+  a.g1 = s * r[0];
+  a.gm = s * gm;
+  a.mg = -s * (r[0] + r[1] + gm);
+  a.hx = s * hx;
+  a.hy = s * hy;
+  a.hx2 = 2.0 * a.hx;
+  a.hy2 = 2.0 * a.hy;
+  a.hz2 = s * 2.0 * hz;
+  a.G = s * 0.5 * (r[0] + r[1] + r[2] + r[3] + gm);
+  return a;
+}
+
+// o += (M (x) I) b on R[i][j] = b[6i+j] (ST = 6, index i) or (I (x) M) b (ST = 1, index j)
+template <int ST>
+__device__ __forceinline__ void apply4_one(const Gen4& a, const double (&b)[36], double (&o)[36]) {
+  constexpr int OS = ST == 6 ? 1 : 6;      // stride of the other index
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int c = OS * k;
+    const double u1 = b[c + ST], u2 = b[c + 2 * ST], u3 = b[c + 3 * ST], u4 = b[c + 4 * ST],
+                 u5 = b[c + 5 * ST];
+    const double u25 = u2 + u5;
+    o[c] = fma(a.g0, u25, o[c]);
+    o[c + ST] = fma(a.g1, u25, fma(a.hy2, u3, fma(-a.hx2, u4, o[c + ST])));
+    o[c + 2 * ST] = fma(a.mg, u2, fma(-a.hy2, u3, fma(a.hx2, u4, fma(a.gm, u5, o[c + 2 * ST]))));
+    o[c + 3 * ST] = fma(a.hy, u2 - u1, fma(-a.G, u3, fma(a.hz2, u4, o[c + 3 * ST])));
+    o[c + 4 * ST] = fma(a.hx, u1 - u2, fma(-a.hz2, u3, fma(-a.G, u4, o[c + 4 * ST])));
+    o[c + 5 * ST] = fma(a.gm, u2, fma(a.mg, u5, o[c + 5 * ST]));
+  }
+}
+
+__device__ __forceinline__ void apply4_V(double vs, const double (&b)[36], double (&o)[36]) {
+#pragma unroll
+  for (int i = 2; i < 6; ++i) {            // S (x) D: rows i = ++ / x / y / --
+    const double w = (i == 2 || i == 5) ? 2.0 * vs : vs;
+    o[6 * i + 4] = fma(w, b[6 * i + 3], o[6 * i + 4]);
+    o[6 * i + 3] = fma(-w, b[6 * i + 4], o[6 * i + 3]);
+  }
+#pragma unroll
+  for (int j = 2; j < 6; ++j) {            // D (x) S: columns j
+    const double w = (j == 2 || j == 5) ? 2.0 * vs : vs;
+    o[6 * 4 + j] = fma(w, b[6 * 3 + j], o[6 * 4 + j]);
+    o[6 * 3 + j] = fma(-w, b[6 * 4 + j], o[6 * 3 + j]);
+  }
+}
+
+template <int PROTO, bool SYM>
+__global__ __launch_bounds__(BLOCK) void lindblad4_cheb_kernel(
+    const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ st, int64_t lds,
+    double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
+  const int64_t gid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = gid < 4 * n;
+  const int64_t i = live ? (gid >> 2) : (n - 1);
+  const int inp = (int)(gid & 3);
+  const int a1 = inp >> 1, a2 = inp & 1;
+  const PointP q = load_point<PROTO>(prm, ldp, i);
+  const double gmA = col(prm, RYD_P_GMJ_A, ldp, i), gmB = col(prm, RYD_P_GMJ_B, ldp, i);
+  const bool valid = point_valid<PROTO>(q, n_steps) && gmA >= 0.0 && gmB >= 0.0 && isfinite(gmA) &&
+                     isfinite(gmB);
+  const int e0 = 6 * a1 + a2;
+  double v[36];
+#pragma unroll
+  for (int e = 0; e < 36; ++e) v[e] = (e == e0) ? 1.0 : 0.0;
+  double nuse = 0.0, nexec = 0.0;
+  bool over_cap = false;
+  const int nseg = n_segments<PROTO>(n_steps);
+  double rsum = 2.0 * (fabs(gmA) + fabs(gmB));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) rsum += fabs(q.gA[c]) + fabs(q.gB[c]);
+  for (int s = 0; s < nseg; ++s) {
+    const Seg g = segment<PROTO>(q, s, n_steps, shape);
+    double emin, emax;
+    h_bounds(g, q.V, q.d1, emin, emax);
+    const double omega = (emax - emin) + rsum;
+    const double x = omega * g.dt;
+    const bool capped = valid && !(x <= X_CAP);
+    const bool active = valid && !capped && x > X_SKIP;
+    over_cap = over_cap || capped;
+    const double sc = active ? 2.0 / omega : 0.0;
+    const Gen4 A = make_gen4(g, q.d1, q.gA, gmA, sc);
+    const Gen4 B = SYM ? A : make_gen4(g, q.d1, q.gB, gmB, sc);
+    const double vs = sc * 0.5 * q.V;
+    cheb_segment<36>(v, x, active,
+                     [&](const double (&b)[36], double (&o)[36]) {
+                       apply4_one<6>(A, b, o);
+                       apply4_one<1>(B, b, o);
+                       apply4_V(vs, b, o);
+                     },
+                     nuse, nexec);
+  }
+  double pop = 0.0;
+#pragma unroll
+  for (int e = 0; e < 36; ++e) pop = (e == e0) ? v[e] : pop;
+  double tr = 0.0;                         // trace: population coordinates {0,1,2,5} x {0,1,2,5}
+#pragma unroll
+  for (int ii = 0; ii < 6; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj)
+      if ((ii < 3 || ii == 5) && (jj < 3 || jj == 5)) tr += v[6 * ii + jj];
+  uint32_t stat = valid ? 0u : RYD_STATUS_BAD_INPUT;
+  if (over_cap) stat |= RYD_STATUS_STEP_CAP;
+  if (!finite_all(v, 36)) stat |= RYD_STATUS_NONFINITE;
+  if (live) {
+#pragma unroll
+    for (int e = 0; e < 36; ++e) st[(int64_t)e * lds + gid] = v[e];
+  }
+  const int lane = threadIdx.x & 63, base = lane & ~3;
+  double p[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) p[x] = lane_get(pop, base + x);
+  const double tr11 = lane_get(tr, base + 3);
+  uint32_t st_all = stat;
+#pragma unroll
+  for (int x = 1; x < 4; ++x) st_all |= (uint32_t)__shfl((int)stat, base + x, 64);
+  if (live && inp == 0) {
+    const double avg = 0.25 * (p[0] + p[1] + p[2] + p[3]);
+    const double nan = __builtin_nan("");
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      sm[(int64_t)(RYD_S_POP0 + x) * ldm + i] = p[x];
+      sm[(int64_t)(RYD_S_OV_RE0 + x) * ldm + i] = nan;
+      sm[(int64_t)(RYD_S_OV_IM0 + x) * ldm + i] = nan;
+    }
+    sm[(int64_t)RYD_S_AVG_POP * ldm + i] = avg;
+    sm[(int64_t)RYD_S_CTRL_PHASE * ldm + i] = nan;
+    sm[(int64_t)RYD_S_PENALTY * ldm + i] = nan;
+    sm[(int64_t)RYD_S_AVG_F * ldm + i] = avg;
+    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = 4.0 * nuse;
+    sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = 4.0 * nexec;
+    sm[(int64_t)RYD_S_TRACE11 * ldm + i] = tr11;
     sm[(int64_t)RYD_S_NSQUARE * ldm + i] = 0.0;
     status[i] = st_all;
   }
@@ -1425,12 +1597,34 @@ using KernelFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, dou
 bool use_propagator(const ryd_batch_desc* d) {
   const bool auto_prop = d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG ||
                          d->protocol == RYD_PROTO_SMOOTH_JP;
-  return d->evolution == RYD_EVOL_LINDBLAD &&
+  return d->dim == 3 && d->evolution == RYD_EVOL_LINDBLAD &&
          (d->method == RYD_METHOD_CHEB_SQUARING || (d->method == RYD_METHOD_CHEBYSHEV && auto_prop));
 }
 
 KernelFn pick_kernel(const ryd_batch_desc* d) {
   const bool sym = (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0;
+  if (d->dim == 4) {
+    if (d->evolution == RYD_EVOL_LINDBLAD) {
+      switch (d->protocol) {
+        case RYD_PROTO_LP_SQUARE:
+          return sym ? lindblad4_cheb_kernel<RYD_PROTO_LP_SQUARE, true> : lindblad4_cheb_kernel<RYD_PROTO_LP_SQUARE, false>;
+        case RYD_PROTO_LP_SHAPED:
+          return sym ? lindblad4_cheb_kernel<RYD_PROTO_LP_SHAPED, true> : lindblad4_cheb_kernel<RYD_PROTO_LP_SHAPED, false>;
+        case RYD_PROTO_BANGBANG:
+          return sym ? lindblad4_cheb_kernel<RYD_PROTO_BANGBANG, true> : lindblad4_cheb_kernel<RYD_PROTO_BANGBANG, false>;
+        case RYD_PROTO_SMOOTH_JP:
+          return sym ? lindblad4_cheb_kernel<RYD_PROTO_SMOOTH_JP, true> : lindblad4_cheb_kernel<RYD_PROTO_SMOOTH_JP, false>;
+      }
+    } else {
+      switch (d->protocol) {
+        case RYD_PROTO_LP_SQUARE: return ket_cheb_kernel<RYD_PROTO_LP_SQUARE, 4>;
+        case RYD_PROTO_LP_SHAPED: return ket_cheb_kernel<RYD_PROTO_LP_SHAPED, 4>;
+        case RYD_PROTO_BANGBANG: return ket_cheb_kernel<RYD_PROTO_BANGBANG, 4>;
+        case RYD_PROTO_SMOOTH_JP: return ket_cheb_kernel<RYD_PROTO_SMOOTH_JP, 4>;
+      }
+    }
+    return nullptr;
+  }
   if (use_propagator(d)) {
     if (d->protocol == RYD_PROTO_LP_SQUARE)
       return sym ? lindblad_prop_kernel<RYD_PROTO_LP_SQUARE, true> : lindblad_prop_kernel<RYD_PROTO_LP_SQUARE, false>;
@@ -1453,10 +1647,10 @@ KernelFn pick_kernel(const ryd_batch_desc* d) {
     }
   } else if (d->evolution == RYD_EVOL_KET) {
     switch (d->protocol) {
-      case RYD_PROTO_LP_SQUARE: return ket_cheb_kernel<RYD_PROTO_LP_SQUARE>;
-      case RYD_PROTO_LP_SHAPED: return ket_cheb_kernel<RYD_PROTO_LP_SHAPED>;
-      case RYD_PROTO_BANGBANG: return ket_cheb_kernel<RYD_PROTO_BANGBANG>;
-      case RYD_PROTO_SMOOTH_JP: return ket_cheb_kernel<RYD_PROTO_SMOOTH_JP>;
+      case RYD_PROTO_LP_SQUARE: return ket_cheb_kernel<RYD_PROTO_LP_SQUARE, 3>;
+      case RYD_PROTO_LP_SHAPED: return ket_cheb_kernel<RYD_PROTO_LP_SHAPED, 3>;
+      case RYD_PROTO_BANGBANG: return ket_cheb_kernel<RYD_PROTO_BANGBANG, 3>;
+      case RYD_PROTO_SMOOTH_JP: return ket_cheb_kernel<RYD_PROTO_SMOOTH_JP, 3>;
     }
   }
   return nullptr;
@@ -1465,7 +1659,9 @@ KernelFn pick_kernel(const ryd_batch_desc* d) {
 int validate(const ryd_batch_desc* d, int64_t n, int64_t ldp, int64_t lds, int64_t ldm) {
   if (!d) return fail(RYD_ERR_INVALID, "desc is NULL");
   if (d->abi_version != RYD_ABI_VERSION) return fail(RYD_ERR_INVALID, "abi_version mismatch");
-  if (d->dim != 3) return fail(RYD_ERR_UNSUPPORTED, "only hilbert_space_dim=3 is implemented");
+  if (d->dim != 3 && d->dim != 4) return fail(RYD_ERR_UNSUPPORTED, "hilbert_space_dim must be 3 or 4");
+  if (d->dim == 4 && d->method != RYD_METHOD_CHEBYSHEV && d->method != RYD_METHOD_CHEB_VECTOR)
+    return fail(RYD_ERR_UNSUPPORTED, "dim 4 runs the Chebyshev state-vector method only");
   if (d->method != RYD_METHOD_CHEBYSHEV && d->method != RYD_METHOD_CHEB_VECTOR &&
       d->method != RYD_METHOD_CHEB_SQUARING && d->method != RYD_METHOD_DOPRI5)
     return fail(RYD_ERR_UNSUPPORTED, "method not implemented");
@@ -1561,6 +1757,7 @@ int launch_coherences(const ryd_batch_desc* d, const double* dp, int64_t n, int6
 
 int validate_coherences(const ryd_batch_desc* d, int64_t n, int64_t ldp, int64_t ldc) {
   if (!d) return fail(RYD_ERR_INVALID, "desc is NULL");
+  if (d->dim != 3) return fail(RYD_ERR_UNSUPPORTED, "process-map coherences: dim 3 only");
   ryd_batch_desc v = *d;                   // the Chebyshev vector method, Lindblad bookkeeping
   v.method = RYD_METHOD_CHEB_VECTOR;
   v.evolution = RYD_EVOL_LINDBLAD;
@@ -1691,8 +1888,10 @@ const char* ryd_last_error(void) { return g_err.c_str(); }
 int ryd_param_count(void) { return RYD_NPARAM; }
 int ryd_summary_width(void) { return RYD_NSUMMARY; }
 int ryd_state_width(int evolution, int dim) {
-  if (dim != 3) return -1;
-  return evolution == RYD_EVOL_LINDBLAD ? 25 : (evolution == RYD_EVOL_KET ? 18 : -1);
+  if (dim != 3 && dim != 4) return -1;
+  if (evolution == RYD_EVOL_LINDBLAD) return dim == 3 ? 25 : 36;
+  if (evolution == RYD_EVOL_KET) return dim == 3 ? 18 : 32;
+  return -1;
 }
 
 int ryd_device_count(int* count) {

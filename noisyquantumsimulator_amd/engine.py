@@ -21,28 +21,36 @@ import numpy as np
 from . import _native as N
 from .physics import DerivedBatch
 
-# single-atom Hermitian basis of the sector: e00, e11, err, ex, ey
-_E = np.zeros((5, 3, 3), dtype=complex)
-_E[0, 0, 0] = 1
-_E[1, 1, 1] = 1
-_E[2, 2, 2] = 1
-_E[3, 1, 2] = _E[3, 2, 1] = 1
-_E[4, 1, 2], _E[4, 2, 1] = 1j, -1j
-# B[5i+j] = e_i (x) e_j  (atom 1 = slow index, as qutip.tensor)
-_B = np.stack([np.kron(_E[i], _E[j]) for i in range(5) for j in range(5)])   # (25, 9, 9)
-_BFLAT = _B.reshape(25, 81)
+def _sector_basis(d: int) -> np.ndarray:
+    """Single-atom Hermitian basis of the sector: e00, e11, err, ex, ey (dim 3), plus
+    e-- = |r-><r-| (dim 4, where r = r+)."""
+    E = np.zeros((5 if d == 3 else 6, d, d), dtype=complex)
+    E[0, 0, 0] = E[1, 1, 1] = E[2, 2, 2] = 1
+    E[3, 1, 2] = E[3, 2, 1] = 1
+    E[4, 1, 2], E[4, 2, 1] = 1j, -1j
+    if d == 4:
+        E[5, 3, 3] = 1
+    # B[k i + j] = e_i (x) e_j  (atom 1 = slow index, as qutip.tensor)
+    k = E.shape[0]
+    return np.stack([np.kron(E[i], E[j]) for i in range(k) for j in range(k)]).reshape(k * k, d ** 4)
 
 
-def expand_rho(state: np.ndarray, n: int) -> np.ndarray:
-    """Compact Lindblad rows (25, >=4n) -> rho[n, 4, 9, 9] (complex128)."""
-    R = np.ascontiguousarray(state[:, :4 * n].T)                # (4n, 25)
-    return (R @ _BFLAT).reshape(n, 4, 9, 9)
+_BFLAT = {3: _sector_basis(3), 4: _sector_basis(4)}
 
 
-def expand_ket(state: np.ndarray, n: int) -> np.ndarray:
-    """Ket rows (18, >=4n) -> psi[n, 4, 9] (complex128)."""
-    s = state[:, :4 * n]
-    return (s[0::2] + 1j * s[1::2]).T.reshape(n, 4, 9)
+def expand_rho(state: np.ndarray, n: int, dim: int = 3) -> np.ndarray:
+    """Compact Lindblad rows (25 or 36, >=4n) -> rho[n, 4, D, D] (complex128), D = dim^2."""
+    B = _BFLAT[dim]
+    R = np.ascontiguousarray(state[:B.shape[0], :4 * n].T)     # (4n, 25 | 36)
+    D = dim * dim
+    return (R @ B).reshape(n, 4, D, D)
+
+
+def expand_ket(state: np.ndarray, n: int, dim: int = 3) -> np.ndarray:
+    """Ket rows (2 D, >=4n) -> psi[n, 4, D] (complex128)."""
+    D = dim * dim
+    s = state[:2 * D, :4 * n]
+    return (s[0::2] + 1j * s[1::2]).T.reshape(n, 4, D)
 
 
 @dataclass
@@ -57,6 +65,7 @@ class EngineResult:
     d2h_ms: float
     matvec_useful: float
     matvec_exec: float
+    dim: int = 3
 
     def col(self, name: str) -> np.ndarray:
         return self.summary[N.S[name]]
@@ -66,11 +75,11 @@ class EngineResult:
 
     def rho(self) -> np.ndarray:
         assert self.evolution == "lindblad"
-        return expand_rho(self.state, self.n)
+        return expand_rho(self.state, self.n, self.dim)
 
     def kets(self) -> np.ndarray:
         assert self.evolution == "ket"
-        return expand_ket(self.state, self.n)
+        return expand_ket(self.state, self.n, self.dim)
 
 
 def protocol_key(batch: DerivedBatch) -> str:
@@ -105,6 +114,10 @@ def pack_params(batch: DerivedBatch, idx: Optional[np.ndarray] = None) -> np.nda
     for key, g in (("G1", g1), ("G0", g0), ("GPHI", gphi), ("GSC", gsc)):
         p[P[key + "_A"]] = g
         p[P[key + "_B"]] = g
+    if batch.dim == 4:
+        gm = batch.mj_rate()[sel]
+        p[P["GMJ_A"]] = gm
+        p[P["GMJ_B"]] = gm
     key = protocol_key(batch)
     if key in ("lp_square", "lp_shaped"):
         p[P["TAU"]] = c["tau_single"][sel]
@@ -159,7 +172,8 @@ def default_n_steps(protocol: str, params: np.ndarray) -> int:
 
 def symmetric_atoms(params: np.ndarray) -> bool:
     P = N.P
-    return all(np.array_equal(params[P[k + "_A"]], params[P[k + "_B"]]) for k in ("G1", "G0", "GPHI", "GSC"))
+    return all(np.array_equal(params[P[k + "_A"]], params[P[k + "_B"]])
+               for k in ("G1", "G0", "GPHI", "GSC", "GMJ"))
 
 
 class Engine:
@@ -191,7 +205,7 @@ class Engine:
 
     def run(self, params: np.ndarray, protocol: str, evolution: str, n_steps: Optional[int] = None,
             shape: str = "square", method: str = "chebyshev", rtol: float = 1e-10,
-            atol: float = 1e-12, max_steps: int = 10 ** 7) -> EngineResult:
+            atol: float = 1e-12, max_steps: int = 10 ** 7, dim: int = 3) -> EngineResult:
         params = np.ascontiguousarray(params, dtype=np.float64)
         if params.shape[0] != N.NPARAM:
             raise ValueError(f"params must have shape ({N.NPARAM}, n)")
@@ -199,8 +213,8 @@ class Engine:
         if n_steps is None:
             n_steps = default_n_steps(protocol, params)
         desc = make_desc(protocol, evolution, n_steps, shape, symmetric_atoms(params), method,
-                         rtol=rtol, atol=atol, max_steps=max_steps)
-        w = N.STATE_WIDTH[evolution]
+                         dim=dim, rtol=rtol, atol=atol, max_steps=max_steps)
+        w = N.STATE_WIDTH_DIM[dim][evolution]
         state = np.zeros((w, 4 * n), dtype=np.float64)
         summ = np.zeros((N.NSUMMARY, n), dtype=np.float64)
         status = np.zeros(n, dtype=np.uint32)
@@ -210,7 +224,7 @@ class Engine:
             self.handle, ctypes.byref(desc), dptr(params), n, n, dptr(state), 4 * n, dptr(summ), n,
             status.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(st)))
         return EngineResult(evolution, n, state, summ, status, st.kernel_ms, st.h2d_ms, st.d2h_ms,
-                            st.matvec_useful, st.matvec_exec)
+                            st.matvec_useful, st.matvec_exec, dim)
 
     def run_coherences(self, params: np.ndarray, protocol: str, n_steps: Optional[int] = None,
                        shape: str = "square") -> Tuple[np.ndarray, np.ndarray]:
@@ -238,15 +252,16 @@ class DeviceBatch:
 
     def __init__(self, engine: Engine, params: np.ndarray, protocol: str, evolution: str,
                  n_steps: Optional[int] = None, shape: str = "square", slot: int = 0,
-                 method: str = "chebyshev"):
+                 method: str = "chebyshev", dim: int = 3):
         self.eng, self.slot = engine, slot
         lib = engine.lib
         params = np.ascontiguousarray(params, dtype=np.float64)
         self.n = n = params.shape[1]
         if n_steps is None:
             n_steps = default_n_steps(protocol, params)
-        self.desc = make_desc(protocol, evolution, n_steps, shape, symmetric_atoms(params), method)
-        self.width = N.STATE_WIDTH[evolution]
+        self.desc = make_desc(protocol, evolution, n_steps, shape, symmetric_atoms(params), method, dim=dim)
+        self.dim = dim
+        self.width = N.STATE_WIDTH_DIM[dim][evolution]
         self.evolution = evolution
         self._bufs = []
 
@@ -283,7 +298,7 @@ class DeviceBatch:
         N.check(lib.ryd_memcpy_d2h(h, s, summ.ctypes.data, self.d_summary, summ.nbytes))
         N.check(lib.ryd_memcpy_d2h(h, s, status.ctypes.data, self.d_status, status.nbytes))
         return EngineResult(self.evolution, self.n, state, summ, status, 0.0, 0.0, 0.0,
-                            summ[N.S["NMV_USEFUL"]].sum(), summ[N.S["NMV_EXEC"]].sum())
+                            summ[N.S["NMV_USEFUL"]].sum(), summ[N.S["NMV_EXEC"]].sum(), self.dim)
 
     def free(self):
         for p in self._bufs:

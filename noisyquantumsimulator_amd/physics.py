@@ -174,6 +174,14 @@ class DerivedBatch:
             return z, z, z, z
         return g1, g0, gphi, gsc
 
+    def mj_rate(self):
+        """dim 4: rate of each of the two mJ-mixing channels |r-><r+|, |r+><r-| per atom
+        (RG/noise_models.py:1287-1295); zero otherwise."""
+        if not self.include_noise or self.dim != 4:
+            return np.zeros(self.n)
+        g = self.cols["mJ_leakage_rate"]
+        return np.where(g > 0, g, 0.0)
+
 
 def _bc(x, n):
     return np.broadcast_to(np.asarray(x, dtype=float), (n,)).astype(float)

@@ -37,6 +37,7 @@ from .constants import KB
 
 LABELS = ("00", "01", "10", "11")
 _IDX = {"00": 0, "01": 1, "10": 3, "11": 4}        # basis index 3*a1 + a2 (dim 3)
+_IDX_DIM = {3: _IDX, 4: {"00": 0, "01": 1, "10": 4, "11": 5}}   # d*a1 + a2
 
 
 # ---------------------------------------------------------------------------
@@ -127,22 +128,23 @@ def compute_CZ_fidelity(results: Dict[str, np.ndarray], extract_global_phase: bo
 
 
 def mixed_phase_penalty(rho: np.ndarray, eigh=None) -> Tuple[np.ndarray, np.ndarray]:
-    """Vectorised dominant-eigenvector controlled phase for rho[n, 4, 9, 9]
+    """Vectorised dominant-eigenvector controlled phase for rho[n, 4, D, D] (D = 9 or 16)
     -> (controlled_phase[n], penalty[n])."""
-    n = rho.shape[0]
+    n, D = rho.shape[0], rho.shape[-1]
+    idx = _IDX_DIM[3 if D == 9 else 4]
     ph = np.zeros((n, 4))
     if eigh == "numpy":
-        w, U = np.linalg.eigh(rho.reshape(-1, 9, 9))
+        w, U = np.linalg.eigh(rho.reshape(-1, D, D))
         k = np.argmax(w, axis=1)
-        vmax = U[np.arange(U.shape[0]), :, k]                    # (4n, 9)
-        comp = np.array([_IDX[l] for l in LABELS] * n)
+        vmax = U[np.arange(U.shape[0]), :, k]                    # (4n, D)
+        comp = np.array([idx[l] for l in LABELS] * n)
         ph = np.angle(vmax[np.arange(4 * n), comp]).reshape(n, 4)
     else:
         eg = _eigh_fn(eigh)
         for i in range(n):
             for k, lab in enumerate(LABELS):
                 w, U = eg(rho[i, k])
-                ph[i, k] = np.angle(U[_IDX[lab], int(np.argmax(w))])
+                ph[i, k] = np.angle(U[idx[lab], int(np.argmax(w))])
     cp = _wrap(ph[:, 3] - ph[:, 1] - ph[:, 2] + ph[:, 0])
     return cp, _penalty(cp)[1]
 
@@ -275,11 +277,10 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                            phase_penalty: str = "reference", eigh=None, return_states: bool = False,
                            devices=None, method: str = "chebyshev") -> BatchResult:
     """Evaluate many simulate_CZ_gate points in one GPU pass (see module doc)."""
-    if hilbert_space_dim != 3:
-        if hilbert_space_dim == 4:
-            raise NotImplementedError("hilbert_space_dim=4 (mJ sublevels) is not yet on the GPU "
-                                      "engine (SURVEY.md §8f item 4)")
+    if hilbert_space_dim not in (3, 4):
         raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
+    dim = hilbert_space_dim
+    D = dim * dim
     from . import engine as E
     b = PH.derive_batch(simulation_inputs, n, species=species, n_rydberg=n_rydberg, qubit_0=qubit_0,
                         qubit_1=qubit_1, hilbert_space_dim=hilbert_space_dim,
@@ -293,7 +294,8 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     nn = b.n
     g = b.channel_rates()
     # mesolve with an empty c_op list evolves kets (RG/simulation.py:683-690)
-    ket_mask = np.all([x == 0 for x in g], axis=0) if include_noise else np.ones(nn, bool)
+    ket_mask = (np.all([x == 0 for x in g], axis=0) & (b.mj_rate() == 0)) if include_noise \
+        else np.ones(nn, bool)
     fids = np.zeros((nn, 4))
     pops = np.zeros((nn, 4))
     cp = np.full(nn, np.nan)
@@ -301,14 +303,15 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     status = np.zeros(nn, np.uint32)
     states = None
     if return_states:
-        states = {"ket": np.zeros((nn, 4, 9), complex), "rho": np.zeros((nn, 4, 9, 9), complex)}
+        states = {"ket": np.zeros((nn, 4, D), complex), "rho": np.zeros((nn, 4, D, D), complex)}
     eng = _engine(devices)
     kms = 0.0
     for evol, mask in (("ket", ket_mask), ("lindblad", ~ket_mask)):
         idx = np.nonzero(mask)[0]
         if idx.size == 0:
             continue
-        r = eng.run(E.pack_params(b, idx), key, evol, shape=shape, method=method)
+        r = eng.run(E.pack_params(b, idx), key, evol, shape=shape,
+                    method=method if dim == 3 else "chebyshev", dim=dim)
         kms += r.kernel_ms
         status[idx] = r.status
         P = r.populations()
@@ -323,7 +326,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
             if need_rho:
                 for s0 in range(0, idx.size, 65536):
                     sl = slice(s0, s0 + 65536)
-                    rho = E.expand_rho(r.state[:, 4 * s0:4 * (s0 + 65536)], min(65536, idx.size - s0))
+                    rho = E.expand_rho(r.state[:, 4 * s0:4 * (s0 + 65536)], min(65536, idx.size - s0), dim)
                     if phase_penalty == "reference":
                         c_, p_ = mixed_phase_penalty(rho, eigh)
                         cp[idx[sl]], pen[idx[sl]] = c_, p_
@@ -412,8 +415,8 @@ def simulate_CZ_gate(
     xi = 1.0
     if is_lp:
         xi = complex(c["xi_re"], c["xi_im"])
-        H1 = OPS.hamiltonian(c["Omega"], c["Delta_gate"], c["V"], 3, d1)
-        H2 = OPS.hamiltonian(c["Omega"] * xi, c["Delta_gate"], c["V"], 3, d1)
+        H1 = OPS.hamiltonian(c["Omega"], c["Delta_gate"], c["V"], hilbert_space_dim, d1)
+        H2 = OPS.hamiltonian(c["Omega"] * xi, c["Delta_gate"], c["V"], hilbert_space_dim, d1)
     rates = {k: c[k] for k in PH.RATE_FIELDS}
     c_ops = OPS.collapse_operators(rates, hilbert_space_dim) if include_noise else []
     noise_breakdown = noise_breakdown_row(b, 0, len(c_ops))

@@ -18,8 +18,8 @@ CALLS = []          # batch sizes seen, for tests that count engine passes
 def point_spec(b, i, n_steps=300):
     c = b.cols
     kw = dict(Omega=c["Omega"][i], V=c["V"][i], delta_zeeman=c["delta_zeeman"][i],
-              delta_stark=c["delta_stark"][i], trap_laser_on=b.trap_laser_on,
-              c_ops=O.collapse_operators({k: c[k][i] for k in O.RATE_KEYS}) if b.include_noise else [])
+              delta_stark=c["delta_stark"][i], trap_laser_on=b.trap_laser_on, dim=b.dim,
+              c_ops=O.collapse_operators({k: c[k][i] for k in O.RATE_KEYS}, b.dim) if b.include_noise else [])
     if b.protocol == "levine_pichler":
         return O.PointSpec(protocol="lp_square", Delta=c["Delta_gate"][i], tau=c["tau_single"][i],
                            xi=complex(c["xi_re"][i], c["xi_im"][i]), **kw)
