@@ -91,6 +91,79 @@ def cpu_baseline(sample: int, procs: int, workload: str = "c2"):
     return json.loads(out.stdout.strip().splitlines()[-1])
 
 
+# C5 (three-atom trajectories) accounting, per include/ryd_engine.h RYD_TS_*:
+# one ladder step = block matvec (124 complex MACs = 992 flops) + norm (108 flops);
+# one block squaring = 8 + 64 + 512 complex MACs (4672 flops) + 168 adds;
+# on-chip reduction = 378 elements x 14 flops per trajectory.
+FLOP_PER_LADDER_STEP = 8 * 124 + 2 * 54
+FLOP_PER_BLOCK_SQUARING = 8 * (8 + 64 + 512) + 2 * 84
+FLOP_PER_TRAJ_REDUCTION = 378 * 14
+C5_BYTES_PER_POINT = 8 * 15 + 8 * (1458 + 729 + 10) + 4   # params read; rho, se, summary, status
+
+
+def run_c5(args, ws, rank, local, pg):
+    """C5: 4096-point (Omega, V/Omega) three-atom blockade grid, 256 quantum-jump
+    trajectories per point, strong-scaled over the ranks (range shards keyed by their
+    global point offset, so the random streams do not depend on N)."""
+    from noisyquantumsimulator_amd import engine as E
+    from noisyquantumsimulator_amd import sweeps as SW
+    from noisyquantumsimulator_amd import trajectories as TR
+    batch, off = SW.c5_rank_shard(rank, ws)
+    params = E.pack_params(batch)
+    n = batch.n
+    eng = E.Engine(devices=[local])
+    db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=args.n_traj,
+                                  seed=20260215, point_offset=off)
+    for _ in range(args.warmup):
+        db.launch()
+    db.synchronize()
+    _barrier(pg)
+    db.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        db.launch()
+    db.synchronize()
+    _barrier(pg)
+    dt = time.perf_counter() - t0
+    dt_max = _max_over_ranks(pg, dt)
+    kms = [db.launch(timed=True) for _ in range(max(3, min(args.steps, 10)))]
+    k_ms = float(np.mean(kms))
+    res = db.fetch()
+    assert np.all(res.status == 0), "engine reported per-point failures"
+    it_use = float(res.col("ITER_USEFUL").sum())
+    it_exec = float(res.col("ITER_EXEC").sum())
+    flops = (it_use * FLOP_PER_LADDER_STEP + float(res.col("NSQUARE").sum()) * FLOP_PER_BLOCK_SQUARING
+             + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
+    achieved_tf = flops / (k_ms * 1e-3) / 1e12
+    achieved_gbs = C5_BYTES_PER_POINT * n / (k_ms * 1e-3) / 1e9
+    total = SW.C5_POINTS * args.steps
+    out = {
+        "metric": "Lindblad param-points/sec (2-atom Rydberg CZ sweep); achieved HBM GB/s vs peak",
+        "value": total / dt_max, "unit": "points/s", "n_gpus": ws, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt_max / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": ("C5: 4096-point (Omega 1-10 MHz x V/Omega 10-1000) three-atom "
+                                f"blockade grid, LP square, {args.n_traj} quantum-jump trajectories "
+                                "per point (Philox4x32-10), |+++> input, medium-apparatus rates"),
+                   "points_per_gpu": n, "global_points": SW.C5_POINTS, "trajectories_per_point": args.n_traj,
+                   "trajectories_per_s": total * args.n_traj / dt_max,
+                   "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS"},
+        "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None, "kernel_ms": k_ms,
+                     "flops_per_launch": flops, "exec_over_useful": it_exec / max(it_use, 1.0),
+                     "mean_jumps": float(res.col("MEAN_JUMPS").mean())},
+        "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_launch": C5_BYTES_PER_POINT * n},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    db.free()
+    eng.close()
+    if pg is not None:
+        pg.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,10 +173,13 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--method", default="chebyshev",
                     choices=["chebyshev", "cheb_squaring", "cheb_vector"])
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--n-traj", type=int, default=256, help="C5 trajectories per point")
     args = ap.parse_args()
 
     ws, rank, local, pg = _dist()
+    if args.workload == "c5":
+        return run_c5(args, ws, rank, local, pg)
     from noisyquantumsimulator_amd import engine as E
     from noisyquantumsimulator_amd import sweeps as SW
 
@@ -161,6 +237,15 @@ def main():
     tr = _measured_traffic(args.workload, args.method, n)
     traffic = tr["bytes_per_launch"] if tr else None
 
+    # the host-buffer form of the boundary (ryd_run_batch: params H2D, kernel, state +
+    # summary D2H) -- PCIe-inclusive, reported beside `value`, never as it
+    t_h = time.perf_counter()
+    rh = eng.run(params, protocol, "lindblad", n_steps=n_steps, method=args.method)
+    t_h = time.perf_counter() - t_h
+    assert np.all(rh.status == 0)
+    host_path = {"points_per_s": n / t_h, "wall_ms": t_h * 1e3, "h2d_ms": rh.h2d_ms,
+                 "kernel_ms": rh.kernel_ms, "d2h_ms": rh.d2h_ms,
+                 "bytes_d2h": 8 * (25 * 4 + 20) * n + 4 * n}
     strong = args.workload == "c4"
     global_points = SW.C4_POINTS if strong else n * ws
     total_points = global_points * args.steps
@@ -182,6 +267,7 @@ def main():
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
                      "traffic": traffic, "kernel_ms": k_ms, "flops_per_launch": flops,
                      "exec_over_useful": res.matvec_exec / max(res.matvec_useful, 1)},
+        "host_path": host_path,
         "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": bytes_per_point * n},

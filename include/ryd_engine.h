@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RYD_ABI_VERSION 2
+#define RYD_ABI_VERSION 3
 
 /* ---- return codes ---- */
 #define RYD_OK              0
@@ -150,6 +150,55 @@ extern "C" {
 #define RYD_C_K3  18
 #define RYD_NCOH  20
 
+/* ---- three-atom blockade, quantum-jump trajectories (ryd_run_trajectories) ----
+ * BASELINE configs[4].  The reference has no 3-atom model; this
+ * build defines it: three identical atoms on an equilateral triangle (pairwise
+ * V P_r(x)P_r), the single-atom H of the two-atom path, the 4 channels per atom
+ * (atom-A rate columns RYD_P_G1_A..GSC_A used for every atom), any protocol
+ * schedule.  Waiting-time Monte-Carlo wave functions: n_traj trajectories per
+ * point, Philox4x32-10 counter RNG keyed (seed; trajectory, jump cycle, global
+ * point index).  Kets: 27 amplitudes, basis 9 a0 + 3 a1 + a2 (a: 0, 1, 2 = r).
+ * Outputs (point-major rows, one per point):
+ *   rho     [n][ld_rho >= RYD_T_RHO_WIDTH]  mean of |psi><psi| over trajectories,
+ *           QuTiP column-stacked vec(rho) as (re, im): element (a, b) at 2 (a + 27 b)
+ *   se      [n][ld_se >= RYD_T_SE_WIDTH]    standard error of element (a, b) at a + 27 b:
+ *           sqrt((mean |X|^2 - |mean X|^2) / (n_traj - 1))
+ *   summary [RYD_T_NSUMMARY][ld_summary]    RYD_TS_* per point
+ *   records [n][n_traj][RYD_T_REC_WIDTH]    optional (NULL = off), per trajectory:
+ *           final normalised ket, jump count, the first RYD_T_REC_JUMPS (time s,
+ *           channel 4 atom + c; c = 0 |1><r|, 1 |0><r|, 2 P_r, 3 P_1), iterations */
+#define RYD_T_DIM          27
+#define RYD_T_RHO_WIDTH    1458
+#define RYD_T_SE_WIDTH     729
+#define RYD_T_LADDER_MAX   40    /* jump times resolved to segment / 2^ladder_levels     */
+#define RYD_T_REC_WIDTH    64
+#define RYD_T_REC_NJUMPS   54
+#define RYD_T_REC_JUMP0    55
+#define RYD_T_REC_JUMPS    4
+#define RYD_T_REC_ITERS    63
+#define RYD_TS_MEAN_JUMPS  0
+#define RYD_TS_FRAC_JUMPED 1
+#define RYD_TS_MAX_JUMPS   2
+#define RYD_TS_TRACE       3     /* trace of the mean rho                               */
+#define RYD_TS_QUBIT_POP   4     /* population left in the 8 qubit states               */
+#define RYD_TS_ITER_USEFUL 5     /* ladder steps, summed over trajectories (flops)      */
+#define RYD_TS_ITER_EXEC   6     /* lane-steps the waves executed (divergence included) */
+#define RYD_TS_NLADDER     7     /* ladders built (one per distinct |Omega|, Delta, dt) */
+#define RYD_TS_NSQUARE     8     /* block squarings performed building them             */
+#define RYD_TS_RESERVED    9
+#define RYD_T_NSUMMARY     10
+
+typedef struct ryd_traj_desc {
+  int32_t abi_version;     /* = RYD_ABI_VERSION */
+  int32_t protocol;        /* RYD_PROTO_* */
+  int32_t shape;           /* RYD_SHAPE_* (LP_SHAPED) */
+  int32_t n_steps;         /* as ryd_batch_desc */
+  int32_t n_traj;          /* trajectories per point: a multiple of 256 */
+  int32_t ladder_levels;   /* 1 .. RYD_T_LADDER_MAX (24 recommended) */
+  uint64_t seed;
+  double psi0[2 * RYD_T_DIM];  /* normalised initial ket, (re, im) interleaved */
+} ryd_traj_desc;
+
 /* ---- per-point status bits ---- */
 #define RYD_STATUS_NONFINITE   1u
 #define RYD_STATUS_STEP_CAP    2u   /* DOPRI5 step cap (ZVODE nsteps analogue)          */
@@ -223,6 +272,24 @@ int ryd_run_coherences_device(ryd_handle* h, int slot, const ryd_batch_desc* des
                               const double* d_params, int64_t n, int64_t ld_params,
                               double* d_coh, int64_t ld_coh, uint32_t* d_status,
                               void* stream, float* elapsed_ms);
+
+/* Three-atom quantum-jump trajectories (layout above).  Host-buffer form:
+ * range-partitions the points over the handle's devices; rho and se are packed
+ * (ld = RYD_T_RHO_WIDTH / RYD_T_SE_WIDTH); records may be NULL.  stats->
+ * matvec_useful / matvec_exec carry the summed RYD_TS_ITER_USEFUL / _EXEC. */
+int ryd_run_trajectories(ryd_handle* h, const ryd_traj_desc* desc,
+                         const double* params, int64_t n, int64_t ld_params,
+                         double* out_rho, double* out_se,
+                         double* out_summary, int64_t ld_summary,
+                         double* out_records, uint32_t* out_status, ryd_stats* stats);
+/* Device form; point_offset = global index of point 0 (the RNG key), so range
+ * shards run by separate processes draw the same streams as one big batch. */
+int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* desc,
+                                const double* d_params, int64_t n, int64_t ld_params,
+                                int64_t point_offset,
+                                double* d_rho, int64_t ld_rho, double* d_se, int64_t ld_se,
+                                double* d_summary, int64_t ld_summary, double* d_records,
+                                uint32_t* d_status, void* stream, float* elapsed_ms);
 
 /* Minimal device-memory plumbing so callers need no other GPU runtime. */
 int ryd_malloc(ryd_handle* h, int slot, size_t bytes, void** d_ptr);

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RYD_ENGINE_LIB") or os.path.join(_HERE, "libryd_engine.so")
 
 # keep in sync with include/ryd_engine.h
-RYD_ABI_VERSION = 2
+RYD_ABI_VERSION = 3
 RYD_OK = 0
 PROTO = {"lp_square": 0, "lp_shaped": 1, "bangbang": 2, "smooth_jp": 3}
 EVOL = {"lindblad": 0, "ket": 1}
@@ -36,9 +36,17 @@ STATE_WIDTH_DIM = {3: STATE_WIDTH, 4: {"lindblad": 36, "ket": 32}}
 C = dict(K0=0, K1=8, K2=16, K3=18)
 NCOH = 20
 
+# three-atom quantum-jump trajectories (ryd_run_trajectories)
+T = dict(DIM=27, RHO_WIDTH=1458, SE_WIDTH=729, LADDER_MAX=40, REC_WIDTH=64, REC_NJUMPS=54,
+         REC_JUMP0=55, REC_JUMPS=4, REC_ITERS=63)
+TS = dict(MEAN_JUMPS=0, FRAC_JUMPED=1, MAX_JUMPS=2, TRACE=3, QUBIT_POP=4, ITER_USEFUL=5,
+          ITER_EXEC=6, NLADDER=7, NSQUARE=8, RESERVED=9)
+T_NSUMMARY = 10
+
 EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary_width",
             "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",
             "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
+            "ryd_run_trajectories", "ryd_run_trajectories_device",
             "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize")
 
 
@@ -49,6 +57,13 @@ class BatchDesc(ctypes.Structure):
                 ("n_steps", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("rtol", ctypes.c_double), ("atol", ctypes.c_double),
                 ("max_steps", ctypes.c_int64)]
+
+
+class TrajDesc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("protocol", ctypes.c_int32),
+                ("shape", ctypes.c_int32), ("n_steps", ctypes.c_int32),
+                ("n_traj", ctypes.c_int32), ("ladder_levels", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("psi0", ctypes.c_double * 54)]
 
 
 class Stats(ctypes.Structure):
@@ -93,6 +108,11 @@ def load() -> ctypes.CDLL:
                                            ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(Stats)]
         lib.ryd_run_coherences_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(BatchDesc), vp, i64,
                                                   i64, vp, i64, vp, vp, ctypes.POINTER(ctypes.c_float)]
+        lib.ryd_run_trajectories.argtypes = [vp, ctypes.POINTER(TrajDesc), dp, i64, i64, dp, dp, dp, i64,
+                                             dp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(Stats)]
+        lib.ryd_run_trajectories_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(TrajDesc), vp, i64, i64,
+                                                    i64, vp, i64, vp, i64, vp, i64, vp, vp, vp,
+                                                    ctypes.POINTER(ctypes.c_float)]
         lib.ryd_malloc.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]
         lib.ryd_free.argtypes = [vp, ctypes.c_int, vp]
         lib.ryd_memcpy_h2d.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]

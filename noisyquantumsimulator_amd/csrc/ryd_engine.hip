@@ -1848,7 +1848,7 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
     (void)hipMemcpy2DAsync(P.p, sizeof(double) * P.cnt, params + P.off, sizeof(double) * ld_params,
                            sizeof(double) * P.cnt, RYD_NPARAM, hipMemcpyHostToDevice, s);
     (void)hipEventRecord(P.b, s);
-    int rc = launch_fn(P.p, P.cnt, P.cnt, P.o, P.st, s);
+    int rc = launch_fn(P.p, P.cnt, P.cnt, P.off, P.o, P.st, s);
     if (rc) {
       cleanup();
       return rc;
@@ -1856,8 +1856,12 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
     (void)hipEventRecord(P.c, s);
     for (int j = 0; j < no; ++j) {
       const int64_t w = (int64_t)outs[j].per_point * P.cnt;
-      (void)hipMemcpy2DAsync(outs[j].host + outs[j].per_point * P.off, sizeof(double) * outs[j].ld, P.o[j],
-                             sizeof(double) * w, sizeof(double) * w, outs[j].rows, hipMemcpyDeviceToHost, s);
+      if (outs[j].rows == 1)       // point-major output: one contiguous slice
+        (void)hipMemcpyAsync(outs[j].host + outs[j].per_point * P.off, P.o[j], sizeof(double) * w,
+                             hipMemcpyDeviceToHost, s);
+      else
+        (void)hipMemcpy2DAsync(outs[j].host + outs[j].per_point * P.off, sizeof(double) * outs[j].ld, P.o[j],
+                               sizeof(double) * w, sizeof(double) * w, outs[j].rows, hipMemcpyDeviceToHost, s);
     }
     (void)hipMemcpyAsync(out_status + P.off, P.st, sizeof(uint32_t) * P.cnt, hipMemcpyDeviceToHost, s);
     (void)hipEventRecord(P.d, s);
@@ -1878,6 +1882,9 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
   if (err != hipSuccess) return fail(RYD_ERR_HIP, std::string("batch: ") + hipGetErrorString(err));
   return RYD_OK;
 }
+
+// three-atom quantum-jump trajectories (BASELINE configs[4])
+#include "ryd_traj.inc"
 
 }  // namespace
 
@@ -2023,7 +2030,7 @@ int ryd_run_batch(ryd_handle* h, const ryd_batch_desc* desc, const double* param
   double kms, hms, dms;
   rc = run_partitioned(
       h, params, n, ld_params, outs, out_status,
-      [&](const double* dp, int64_t cnt, int64_t ldp, const std::vector<double*>& o, uint32_t* dst,
+      [&](const double* dp, int64_t cnt, int64_t ldp, int64_t, const std::vector<double*>& o, uint32_t* dst,
           hipStream_t s) { return launch(desc, dp, cnt, ldp, o[0], 4 * cnt, o[1], cnt, dst, s); },
       kms, hms, dms);
   if (rc) return rc;
@@ -2055,7 +2062,7 @@ int ryd_run_coherences(ryd_handle* h, const ryd_batch_desc* desc, const double* 
   double kms, hms, dms;
   rc = run_partitioned(
       h, params, n, ld_params, outs, out_status,
-      [&](const double* dp, int64_t cnt, int64_t ldp, const std::vector<double*>& o, uint32_t* dst,
+      [&](const double* dp, int64_t cnt, int64_t ldp, int64_t, const std::vector<double*>& o, uint32_t* dst,
           hipStream_t s) { return launch_coherences(desc, dp, cnt, ldp, o[0], cnt, dst, s); },
       kms, hms, dms);
   if (rc) return rc;
@@ -2066,6 +2073,78 @@ int ryd_run_coherences(ryd_handle* h, const ryd_batch_desc* desc, const double* 
     stats->matvec_useful = stats->matvec_exec = 0.0;
     stats->n_devices = (int)h->dev.size();
     stats->reserved = 0;
+  }
+  return RYD_OK;
+}
+
+int ryd_run_trajectories(ryd_handle* h, const ryd_traj_desc* desc, const double* params, int64_t n,
+                         int64_t ld_params, double* out_rho, double* out_se, double* out_summary,
+                         int64_t ld_summary, double* out_records, uint32_t* out_status, ryd_stats* stats) {
+  if (!h) return fail(RYD_ERR_INVALID, "handle is NULL");
+  int rc = validate_traj(desc, n, ld_params);
+  if (rc) return rc;
+  if (ld_summary < n) return fail(RYD_ERR_INVALID, "leading dimension too small");
+  if (n > 0 && (!params || !out_rho || !out_se || !out_summary || !out_status))
+    return fail(RYD_ERR_INVALID, "NULL buffer");
+  // point-major rows: one "row" of width*cnt doubles per shard
+  std::vector<HostOut> outs = {{out_rho, RYD_T_RHO_WIDTH, 1, RYD_T_RHO_WIDTH},
+                               {out_se, RYD_T_SE_WIDTH, 1, RYD_T_SE_WIDTH},
+                               {out_summary, ld_summary, RYD_T_NSUMMARY, 1}};
+  if (out_records) outs.push_back({out_records, 0, 1, RYD_T_REC_WIDTH * desc->n_traj});
+  double kms, hms, dms;
+  rc = run_partitioned(
+      h, params, n, ld_params, outs, out_status,
+      [&](const double* dp, int64_t cnt, int64_t ldp, int64_t off, const std::vector<double*>& o,
+          uint32_t* dst, hipStream_t s) {
+        return launch_traj(desc, dp, cnt, ldp, off, o[0], RYD_T_RHO_WIDTH, o[1], RYD_T_SE_WIDTH, o[2], cnt,
+                           out_records ? o[3] : nullptr, dst, s);
+      },
+      kms, hms, dms);
+  if (rc) return rc;
+  if (stats) {
+    stats->kernel_ms = kms;
+    stats->h2d_ms = hms;
+    stats->d2h_ms = dms;
+    double u = 0.0, x = 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+      u += out_summary[(int64_t)RYD_TS_ITER_USEFUL * ld_summary + i];
+      x += out_summary[(int64_t)RYD_TS_ITER_EXEC * ld_summary + i];
+    }
+    stats->matvec_useful = u;
+    stats->matvec_exec = x;
+    stats->n_devices = (int)h->dev.size();
+    stats->reserved = 0;
+  }
+  return RYD_OK;
+}
+
+int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* desc, const double* d_params,
+                                int64_t n, int64_t ld_params, int64_t point_offset, double* d_rho,
+                                int64_t ld_rho, double* d_se, int64_t ld_se, double* d_summary,
+                                int64_t ld_summary, double* d_records, uint32_t* d_status, void* stream,
+                                float* elapsed_ms) {
+  if (!h || slot < 0 || slot >= (int)h->dev.size()) return fail(RYD_ERR_INVALID, "bad handle/slot");
+  int rc = validate_traj(desc, n, ld_params);
+  if (rc) return rc;
+  if (ld_rho < RYD_T_RHO_WIDTH || ld_se < RYD_T_SE_WIDTH || ld_summary < n || point_offset < 0)
+    return fail(RYD_ERR_INVALID, "leading dimension too small or negative point_offset");
+  HIPCHK(hipSetDevice(h->dev[slot]));
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream[slot];
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (elapsed_ms) {
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+  }
+  rc = launch_traj(desc, d_params, n, ld_params, point_offset, d_rho, ld_rho, d_se, ld_se, d_summary, ld_summary,
+                   d_records, d_status, s);
+  if (rc) return rc;
+  if (elapsed_ms) {
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(elapsed_ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
   }
   return RYD_OK;
 }

@@ -108,6 +108,42 @@ def species_temperature_power_grid(n_T: int = 1000, n_P: int = 500, include_nois
                            include_noise=include_noise)
 
 
+C5_SHAPE = (64, 64)                # Omega x V/Omega
+C5_POINTS = 64 * 64
+
+
+def blockade_grid_3atom(n_omega: int = 64, n_vo: int = 64, include_noise: bool = True,
+                        point_slice: Optional[slice] = None) -> PH.DerivedBatch:
+    """C5: Omega/2pi in linspace(1, 10) MHz x V/Omega in logspace(10, 1000),
+    LP square, medium apparatus.  Omega is set the physical way (480 nm leg power,
+    Omega ∝ sqrt(P2)) and V/Omega through the atom spacing (V = C6/R^6, via
+    spacing_factor), so the LP (Delta/Omega, Omega tau) lookup, xi and every noise rate
+    follow from the reference formulas per point.  Point order: Omega-major.  The
+    three-atom engine uses these two-atom columns for each atom and each pair."""
+    warnings.simplefilter("ignore")
+    exc = medium_excitation()
+    ref = PH.derive_batch(CF.LPSimulationInputs(excitation=exc), **_apparatus_kwargs(), include_noise=False)
+    om0, V0 = ref["Omega"][0], ref["V"][0]
+    om = 2 * np.pi * 1e6 * np.linspace(1, 10, n_omega)
+    vo = np.logspace(1, 3, n_vo)
+    OM, VO = np.meshgrid(om, vo, indexing="ij")
+    OM, VO = OM.ravel(), VO.ravel()
+    if point_slice is not None:
+        OM, VO = OM[point_slice], VO[point_slice]
+    p2 = MEDIUM["laser_2_power"] * (OM / om0) ** 2
+    sf = MEDIUM["spacing_factor"] * (V0 / (VO * OM)) ** (1.0 / 6.0)
+    return PH.derive_batch(CF.LPSimulationInputs(excitation=exc), n=OM.size,
+                           **_apparatus_kwargs(spacing_factor=sf), include_noise=include_noise,
+                           overrides=dict(laser_2_power=p2))
+
+
+def c5_rank_shard(rank: int, world_size: int, include_noise: bool = True):
+    """Strong-scaling shard of the fixed 4096-point C5 grid: (batch, global offset of
+    its first point) -- the offset keys the trajectories' random streams."""
+    sl = range_shard(C5_POINTS, rank, world_size)
+    return blockade_grid_3atom(include_noise=include_noise, point_slice=sl), sl.start
+
+
 def range_shard(n: int, rank: int, world_size: int) -> slice:
     """Contiguous range partition: point i -> rank floor(world_size * i / n)."""
     if not 0 <= rank < world_size:

@@ -1,0 +1,174 @@
+"""Three-atom blockade with quantum-jump trajectories (C5) on the GPU, through the
+C-ABI (ryd_run_trajectories), against the CPU oracle (oracle/three_atom_oracle.py):
+
+* rates = 0: every trajectory is the Schrodinger ket -> mean rho exact to 1e-10, se = 0;
+* atom parked in |0>: equals the two-atom GPU ket engine;
+* noisy: mean rho within 5.5 standard errors of the exact 729x729 Liouvillian state;
+* single trajectories: same jump count / channels, jump times within the ladder
+  quantum, same final ket as the exact-jump-time oracle on the same Philox stream;
+* launch-shape independence (bit-exact), bad inputs, full 4096-point C5 grid properties.
+"""
+import warnings
+
+import numpy as np
+import pytest
+
+from noisyquantumsimulator_amd import _native as N
+from noisyquantumsimulator_amd import configurations as CF
+from noisyquantumsimulator_amd import engine as E
+from noisyquantumsimulator_amd import physics as PH
+from noisyquantumsimulator_amd import sweeps as SW
+from noisyquantumsimulator_amd import trajectories as TR
+from oracle import three_atom_oracle as O3
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(species="Rb87", n_rydberg=70, tweezer_power=0.020, tweezer_waist=0.8e-6, temperature=2e-6,
+          spacing_factor=2.8, B_field=1e-4, NA=0.5)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return E.Engine()
+
+
+def _c5(idx, scale=1.0):
+    warnings.simplefilter("ignore")
+    p = E.pack_params(SW.blockade_grid_3atom(point_slice=slice(0, SW.C5_POINTS)))[:, idx].copy()
+    p[4:12] *= scale
+    return np.ascontiguousarray(p)
+
+
+def _two_atom(si, n=2):
+    warnings.simplefilter("ignore")
+    exc = SW.medium_excitation()
+    b = PH.derive_batch(si(excitation=exc), n, **dict(KW, temperature=np.linspace(2e-6, 5e-6, n)))
+    return E.pack_params(b)
+
+
+@pytest.mark.parametrize("protocol,n_steps,shape", [("lp_square", None, "square"), ("bangbang", None, "square"),
+                                                    ("smooth_jp", 60, "square"), ("lp_shaped", 40, "cosine")])
+def test_zero_rates_equal_pure_evolution(eng, protocol, n_steps, shape):
+    if protocol == "lp_square":
+        p = _c5([0, 700, 2100, 4095])
+    elif protocol == "bangbang":
+        p = _two_atom(CF.JPSimulationInputs)
+    elif protocol == "smooth_jp":
+        p = _two_atom(CF.SmoothJPSimulationInputs)
+    else:
+        p = _two_atom(lambda excitation: CF.LPSimulationInputs(excitation=excitation, pulse_shape="cosine"))
+    p[4:12] = 0.0
+    ns = n_steps if n_steps is not None else E.default_n_steps(protocol, p)
+    psi0 = TR.plus_state()
+    r = TR.run_trajectories(eng, p, protocol, psi0, n_traj=256, n_steps=ns, shape=shape)
+    assert np.all(r.status == 0)
+    assert np.all(r.col("MEAN_JUMPS") == 0)
+    for i in range(p.shape[1]):
+        psi = O3.pure_ket(p[:, i], protocol, psi0, n_steps=ns, shape=shape)
+        np.testing.assert_allclose(r.rho[i], np.outer(psi, psi.conj()), atol=1e-10, rtol=0, err_msg=f"{protocol}/{i}")
+        assert r.se[i].max() < 1e-12
+    np.testing.assert_allclose(r.col("TRACE"), 1.0, atol=1e-12)
+
+
+def test_spectator_atom_matches_two_atom_engine(eng):
+    p = _c5([10, 3000])
+    p[4:12] = 0.0
+    k2 = eng.run(p, "lp_square", "ket").kets()               # two-atom GPU ket path
+    one, zero = np.array([0, 1, 0]), np.array([1, 0, 0])
+    r = TR.run_trajectories(eng, p, "lp_square", TR.product_ket(one, one, zero), n_traj=256)
+    for i in range(2):
+        psi = np.kron(k2[i, 3], zero)                        # input |11> (label index 3) (x) |0>
+        np.testing.assert_allclose(r.rho[i], np.outer(psi, psi.conj()), atol=1e-10, rtol=0)
+
+
+def test_noisy_mean_rho_within_standard_error(eng):
+    idx = [5, 1800, 4000]
+    p = _c5(idx, scale=30.0)
+    psi0 = TR.plus_state()
+    r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=2048, seed=20260215)
+    assert np.all(r.status == 0)
+    assert np.all(r.col("MEAN_JUMPS") > 0.05)
+    np.testing.assert_allclose(r.col("TRACE"), 1.0, atol=1e-12)
+    z2 = []
+    for i in range(len(idx)):
+        ref = O3.exact_rho(p[:, i], "lp_square", psi0)
+        d = np.abs(r.rho[i] - ref)
+        # rare-channel elements may have no sampled event: Poisson floor sqrt(|rho| / n)
+        se = np.maximum(r.se[i], np.sqrt(np.abs(ref) / 2048))
+        ok = (d < 1e-9) | (d < 5.5 * se + 1e-8)
+        assert ok.all(), (i, (d / np.maximum(se, 1e-300)).max())
+        m = r.se[i] > 1e-4
+        z2.append(((d[m] / r.se[i][m]) ** 2).mean())
+    assert 0.3 < np.mean(z2) < 2.0, z2                        # the errors ARE standard errors
+
+
+def test_trajectories_match_exact_time_oracle(eng):
+    """One-to-one: same Philox stream -> same jumps and final ket as the CPU unravelling
+    with exact (root-found) jump times; the GPU resolves jump times to dt / 2^L."""
+    L = 36
+    p = _c5([1200], scale=40.0)
+    psi0 = TR.plus_state()
+    r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=256, seed=77, ladder_levels=L, records=True)
+    assert r.status[0] == 0
+    nj, tj, cj, kets = r.n_jumps()[0], r.jump_times()[0], r.jump_channels()[0], r.kets()[0]
+    dt = p[N.P["TAU"], 0]
+    checked = 0
+    for t in range(24):
+        k, jumps = O3.mc_trajectory(p[:, 0], "lp_square", psi0, point=0, traj=t, seed=77)
+        assert nj[t] == len(jumps), t
+        for m, (tt, ch) in enumerate(jumps[:N.T["REC_JUMPS"]]):
+            assert cj[t, m] == ch
+            assert tt - 1e-18 <= tj[t, m] <= tt + 2 * dt * 2.0 ** -L + 1e-18
+            checked += 1
+        assert abs(np.vdot(k, kets[t])) > 1 - 1e-8, t
+    assert checked > 5
+
+
+def test_launch_shape_and_partition_independence(eng):
+    p = _c5(list(range(0, 4096, 512)), scale=20.0)
+    a = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5, records=True)
+    b = TR.run_trajectories(eng, p, "lp_square", n_traj=512, seed=5, records=True)
+    np.testing.assert_array_equal(a.records, b.records[:, :256])     # a trajectory = its stream
+    c = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5)
+    np.testing.assert_array_equal(a.rho, c.rho)                         # deterministic
+    # two device-side range shards with their global offsets == one batch
+    outs = []
+    for lo, hi in ((0, 3), (3, 8)):
+        db = TR.TrajectoryDeviceBatch(eng, p[:, lo:hi], "lp_square", n_traj=256, seed=5, point_offset=lo)
+        db.launch()
+        db.synchronize()
+        outs.append(db.fetch())
+        db.free()
+    np.testing.assert_array_equal(np.concatenate([o.rho for o in outs]), a.rho)
+    d = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=6)
+    assert not np.array_equal(d.rho, a.rho)
+
+
+def test_bad_inputs(eng):
+    p = _c5([1, 2, 3])
+    p[N.P["OMEGA"], 1] = 0.0
+    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256)
+    assert r.status[1] & N.STATUS_BAD_INPUT and r.status[0] == 0 and r.status[2] == 0
+    assert np.all(r.rho[1] == 0)
+    with pytest.raises(N.EngineError):
+        TR.run_trajectories(eng, p, "lp_square", n_traj=100)
+    with pytest.raises(N.EngineError):
+        TR.run_trajectories(eng, p, "lp_square", n_traj=256, ladder_levels=0)
+
+
+def test_c5_full_grid_properties(eng):
+    warnings.simplefilter("ignore")
+    p = E.pack_params(SW.blockade_grid_3atom())
+    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=20260215)
+    assert r.n == 4096 and np.all(r.status == 0)
+    np.testing.assert_allclose(r.col("TRACE"), 1.0, atol=1e-12)
+    np.testing.assert_allclose(r.rho, np.conj(np.transpose(r.rho, (0, 2, 1))), atol=0)
+    assert np.linalg.eigvalsh(r.rho).min() > -1e-12
+    q = r.col("QUBIT_POP")
+    assert np.all((q > 0.5) & (q <= 1 + 1e-12))
+    assert np.all(np.isfinite(r.se))
+    psi0 = TR.plus_state()
+    for i in (77, 3333):
+        ref = O3.exact_rho(p[:, i], "lp_square", psi0)
+        d = np.abs(r.rho[i] - ref)
+        assert np.all((d < 1e-9) | (d < 5.5 * np.maximum(r.se[i], np.sqrt(np.abs(ref) / 256)) + 1e-8))

@@ -35,6 +35,13 @@ def test_header_constants_match_binding():
     for k, v in N.PROTO.items():
         assert int(defs["RYD_PROTO_" + k.upper()]) == v
     assert ctypes.sizeof(N.BatchDesc) == 56 and ctypes.sizeof(N.Stats) == 48
+    for k, v in N.T.items():
+        assert int(defs["RYD_T_" + k]) == v
+    for k, v in N.TS.items():
+        assert int(defs["RYD_TS_" + k]) == v
+    assert int(defs["RYD_T_NSUMMARY"]) == N.T_NSUMMARY
+    assert int(defs["RYD_ABI_VERSION"]) == N.RYD_ABI_VERSION
+    assert ctypes.sizeof(N.TrajDesc) == 464
 
 
 def test_library_loads_and_exports():
@@ -43,7 +50,7 @@ def test_library_loads_and_exports():
     lib = N.load()
     for sym in N.EXPORTED:
         assert hasattr(lib, sym), sym
-    assert lib.ryd_abi_version() == N.RYD_ABI_VERSION == 2
+    assert lib.ryd_abi_version() == N.RYD_ABI_VERSION == 3
     assert lib.ryd_param_count() == N.NPARAM
     assert lib.ryd_summary_width() == N.NSUMMARY
     assert lib.ryd_state_width(0, 3) == 25 and lib.ryd_state_width(1, 3) == 18
