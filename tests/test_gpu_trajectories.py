@@ -118,8 +118,11 @@ def test_trajectories_match_exact_time_oracle(eng):
         assert nj[t] == len(jumps), t
         for m, (tt, ch) in enumerate(jumps[:N.T["REC_JUMPS"]]):
             assert cj[t, m] == ch
-            assert tt - 1e-18 <= tj[t, m] <= tt + 2 * dt * 2.0 ** -L + 1e-18
-            checked += 1
+            if m == 0:     # first jump: exactly the quantum that contains the crossing
+                assert tt - 1e-20 <= tj[t, m] <= tt + dt * 2.0 ** -L + 1e-20
+                checked += 1
+            else:          # later ones inherit the O(quantum) shift of the state before them
+                assert abs(tj[t, m] - tt) <= 1e-9 * tt
         assert abs(np.vdot(k, kets[t])) > 1 - 1e-8, t
     assert checked > 5
 
