@@ -136,6 +136,8 @@ def run_c5(args, ws, rank, local, pg):
              + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     achieved_gbs = C5_BYTES_PER_POINT * n / (k_ms * 1e-3) / 1e9
+    tr = _measured_traffic("c5", "mcwf", n) if args.n_traj == 256 else None
+    traffic = tr["bytes_per_launch"] if tr else None
     total = SW.C5_POINTS * args.steps
     out = {
         "metric": "Lindblad param-points/sec (2-atom Rydberg CZ sweep); achieved HBM GB/s vs peak",
@@ -149,11 +151,11 @@ def run_c5(args, ws, rank, local, pg):
                    "trajectories_per_s": total * args.n_traj / dt_max,
                    "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS"},
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None, "kernel_ms": k_ms,
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel_ms": k_ms,
                      "flops_per_launch": flops, "exec_over_useful": it_exec / max(it_use, 1.0),
                      "mean_jumps": float(res.col("MEAN_JUMPS").mean())},
         "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": C5_BYTES_PER_POINT * n},
     }
     if rank == 0:
