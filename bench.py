@@ -1,6 +1,6 @@
 """Benchmark: Lindblad parameter points/s on the C2 sweep (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4]
+    python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4|c5]
 
 A step = one propagation of this rank's 10,000-point LP-square (Omega, Delta)
 sweep -- every point's 4 basis density matrices through both pulses, noise
@@ -8,8 +8,10 @@ rates from the reference formulas -- with inputs resident in HBM.  ``--workload
 c3`` runs the 100k-point smooth-JP (Omega, Omega*tau) Pareto sweep instead
 (300 reference segments per point); ``--workload c4`` the 1M-point species x
 temperature x tweezer-power LP-square grid (BASELINE configs[3]), range-sharded
-over the ranks (strong scaling: the global grid is fixed).  Both are secondary
-lines, not the metric.  With N > 1
+over the ranks (strong scaling: the global grid is fixed); ``--workload c5`` the
+4096-point three-atom blockade grid with 256 quantum-jump trajectories per point
+(BASELINE configs[4]), strong-scaled the same way.  These are secondary lines,
+not the metric.  With N > 1
 ranks (torch.distributed.run, one process per GPU) the global sweep is N x 10k
 points range-partitioned by Delta/Omega; no collective touches the data path
 (weak scaling); a gloo barrier brackets the timed region and the max time over
@@ -158,6 +160,9 @@ def run_c5(args, ws, rank, local, pg):
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": C5_BYTES_PER_POINT * n},
     }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        procs = max(1, min(16, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(min(args.cpu_sample, 64), procs, "c5")
     if rank == 0:
         print(json.dumps(out), flush=True)
     db.free()
@@ -274,9 +279,11 @@ def main():
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": bytes_per_point * n},
     }
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.workload in ("c2", "c4"):
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         procs = max(1, min(16, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, procs, args.workload)
+        # C3 points cost ~6 core-seconds each on the CPU path: a smaller sample
+        sample = args.cpu_sample if args.workload != "c3" else min(args.cpu_sample, 32)
+        out["cpu_baseline"] = cpu_baseline(sample, procs, args.workload)
     if rank == 0:
         print(json.dumps(out), flush=True)
     db.free()

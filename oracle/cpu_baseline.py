@@ -31,13 +31,35 @@ def _one(spec):
     return O.run_point(spec, method="zvode")
 
 
+def _one_c5(args):
+    """All trajectories of one C5 point through the exact-jump-time unravelling."""
+    from oracle import three_atom_oracle as O3
+    p, point, n_traj, psi0 = args
+    for t in range(n_traj):
+        O3.mc_trajectory(p, "lp_square", psi0, point=point, traj=t, seed=20260215)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sample", type=int, default=96)
     ap.add_argument("--procs", type=int, default=8)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--n-traj", type=int, default=256)
     a = ap.parse_args()
     from noisyquantumsimulator_amd import sweeps as SW
+    if a.workload == "c5":
+        return main_c5(a, SW)
+    if a.workload == "c3":
+        b = SW.pareto_tgate_grid()
+        idx = np.linspace(0, b.n - 1, a.sample).astype(int)
+        c = b.cols
+        specs = [O.PointSpec(protocol="smooth_jp", Omega=c["Omega"][i], V=c["V"][i], Delta=c["Delta_seg"][i],
+                             tau=c["tau_total"][i], A=c["A"][i], omega_mod=c["omega_mod"][i],
+                             phi_offset=c["phi_offset"][i], n_steps=300, delta_zeeman=c["delta_zeeman"][i],
+                             delta_stark=c["delta_stark"][i],
+                             c_ops=O.collapse_operators({k: c[k][i] for k in O.RATE_KEYS}))
+                 for i in idx]
+        return _time(a, specs, "the C3 100k smooth-JP sweep (300 segments, ZVODE restarted per segment)")
     if a.workload == "c2":
         b = SW.omega_delta_grid()
         idx = np.linspace(0, b.n - 1, a.sample).astype(int)
@@ -54,6 +76,10 @@ def main():
                          delta_zeeman=c["delta_zeeman"][i], delta_stark=c["delta_stark"][i],
                          c_ops=O.collapse_operators({k: c[k][i] for k in O.RATE_KEYS}))
              for i in idx]
+    _time(a, specs, what)
+
+
+def _time(a, specs, what):
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(a.procs) as pool:
         pool.map(_one, specs, chunksize=1)
@@ -63,6 +89,24 @@ def main():
         sample=f"{a.sample} points evenly spaced over {what}; oracle ZVODE-Adams "
                f"restatement of qutip.mesolve (atol 1e-10, rtol 1e-8, reference tlists); "
                f"{a.procs} single-threaded worker processes; {wall:.2f} s wall")))
+
+
+def main_c5(a, SW):
+    from noisyquantumsimulator_amd import engine as E
+    from noisyquantumsimulator_amd import trajectories as TR
+    full = np.linspace(0, SW.C5_POINTS - 1, a.sample).astype(int)
+    p = E.pack_params(SW.blockade_grid_3atom())
+    jobs = [(p[:, i].copy(), int(i), a.n_traj, TR.plus_state()) for i in full]
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(a.procs) as pool:
+        pool.map(_one_c5, jobs, chunksize=1)
+    wall = time.perf_counter() - t0
+    print(json.dumps(dict(
+        value=a.sample / wall, unit="points/s", cores=a.procs, kind="port",
+        sample=f"{a.sample} points evenly spaced over the C5 4096-point grid, {a.n_traj} "
+               f"trajectories each through the oracle's exact-jump-time MCWF unravelling "
+               f"(scipy expm + brentq, the same Philox streams); {a.procs} single-threaded "
+               f"worker processes; {wall:.2f} s wall")))
 
 
 if __name__ == "__main__":
