@@ -341,23 +341,40 @@ __device__ __forceinline__ void apply_K(const KGen& k, const double (&b)[18], do
 template <int NV, typename Apply>
 __device__ __forceinline__ void cheb_segment(double (&v)[NV], double x, bool active, Apply apply2Y,
                                              double& nuse, double& nexec) {
-  int ks = active ? cheb_terms(x) + MILLER_MARGIN : -1;
+  const int kt = active ? cheb_terms(x) : -1;   // series terms that matter (tail < 1e-17)
+  int ks = active ? kt + MILLER_MARGIN : -1;    // Miller's recurrence starts higher
   int kmax = wave_max(ks);
   kmax = __builtin_amdgcn_readfirstlane(kmax);
   if (kmax < 0) return;                      // whole wave skips this segment
   const int kstart = (kmax + 1) & ~1;        // even
+  int kc = wave_max(kt);
+  kc = __builtin_amdgcn_readfirstlane(kc);
+  const int kcut = (kc + 1) & ~1;            // even; Clenshaw vectors from here down
   const double i2x = active ? 2.0 / x : 0.0;
   double bA[NV], bB[NV];
 #pragma unroll
   for (int e = 0; e < NV; ++e) bA[e] = bB[e] = 0.0;
   double Jp1 = 0.0, Jp2 = 0.0, S = 0.0;
-  for (int k = kstart; k >= 2; k -= 2) {
+  // the margin: Bessel recurrence only (the coefficients there are below 1e-17 of
+  // the sum, so their Clenshaw vector updates are skipped)
+  for (int k = kstart; k > kcut; k -= 2) {
+    const double Jk = fma(i2x * (double)(k + 1), Jp1, -Jp2) + (k == ks ? MILLER_SEED : 0.0);
+    Jp2 = Jp1;
+    Jp1 = Jk;
+    S = fma(2.0, Jk, S);
+    const double Jk1 = fma(i2x * (double)k, Jp1, -Jp2) + (k - 1 == ks ? MILLER_SEED : 0.0);
+    Jp2 = Jp1;
+    Jp1 = Jk1;
+  }
+  for (int k = kcut; k >= 2; k -= 2) {
     // step k (even): bB <- a_k v + 2Y bA + bB
     double Jk = fma(i2x * (double)(k + 1), Jp1, -Jp2) + (k == ks ? MILLER_SEED : 0.0);
     Jp2 = Jp1;
     Jp1 = Jk;
     S = fma(2.0, Jk, S);
-    const double ck = 2.0 * Jk;
+    // terms above this lane's own cut stay out, so a point's result does not depend
+    // on its wave neighbours (bit for bit)
+    const double ck = k <= kt ? 2.0 * Jk : 0.0;
 #pragma unroll
     for (int e = 0; e < NV; ++e) bB[e] = fma(ck, v[e], bB[e]);
     apply2Y(bA, bB);
@@ -365,7 +382,7 @@ __device__ __forceinline__ void cheb_segment(double (&v)[NV], double x, bool act
     double Jk1 = fma(i2x * (double)k, Jp1, -Jp2) + (k - 1 == ks ? MILLER_SEED : 0.0);
     Jp2 = Jp1;
     Jp1 = Jk1;
-    const double ck1 = 2.0 * Jk1;
+    const double ck1 = k - 1 <= kt ? 2.0 * Jk1 : 0.0;
 #pragma unroll
     for (int e = 0; e < NV; ++e) bA[e] = fma(ck1, v[e], bA[e]);
     apply2Y(bB, bA);
@@ -383,9 +400,9 @@ __device__ __forceinline__ void cheb_segment(double (&v)[NV], double x, bool act
     const double inv = 1.0 / S;
 #pragma unroll
     for (int e = 0; e < NV; ++e) v[e] = bB[e] * inv;
-    nuse += (double)(ks + 1);
+    nuse += (double)(kt + 1);
   }
-  nexec += (double)(kstart + 1);
+  nexec += (double)(kcut + 1);
 }
 
 // ---------------------------------------------------------------------------
