@@ -102,6 +102,28 @@ def test_noisy_mean_rho_within_standard_error(eng):
     assert 0.3 < np.mean(z2) < 2.0, z2                        # the errors ARE standard errors
 
 
+@pytest.mark.parametrize("protocol,n_steps", [("bangbang", None), ("smooth_jp", 12)])
+def test_noisy_multi_segment_protocols(eng, protocol, n_steps):
+    """Bang-bang rebuilds the ladder every segment (different lengths) inside the
+    jumper rounds; smooth JP rotates the frame every segment."""
+    p = _two_atom(CF.JPSimulationInputs if protocol == "bangbang" else CF.SmoothJPSimulationInputs, n=1)
+    p[4:12] *= 5.0                                            # ~1-2 jumps per trajectory
+    ns = n_steps if n_steps is not None else E.default_n_steps(protocol, p)
+    psi0 = TR.plus_state()
+    r = TR.run_trajectories(eng, p, protocol, psi0, n_traj=2048, seed=99, n_steps=ns, records=True)
+    assert r.status[0] == 0 and r.col("MEAN_JUMPS")[0] > 0.05
+    ref = O3.exact_rho(p[:, 0], protocol, psi0, n_steps=ns)
+    d = np.abs(r.rho[0] - ref)
+    se = np.maximum(r.se[0], np.sqrt(np.abs(ref) / 2048))
+    assert np.all((d < 1e-9) | (d < 5.5 * se + 1e-8)), (d / se).max()
+    # and one-to-one against the exact-jump-time oracle for a few trajectories
+    nj, cj, kets = r.n_jumps()[0], r.jump_channels()[0], r.kets()[0]
+    for t in range(6):
+        k, jumps = O3.mc_trajectory(p[:, 0], protocol, psi0, point=0, traj=t, seed=99, n_steps=ns)
+        assert nj[t] == len(jumps) and all(cj[t, m] == ch for m, (_, ch) in enumerate(jumps[:4]))
+        assert abs(np.vdot(k, kets[t])) > 1 - 1e-6
+
+
 def test_trajectories_match_exact_time_oracle(eng):
     """One-to-one: same Philox stream -> same jumps and final ket as the CPU unravelling
     with exact (root-found) jump times; the GPU resolves jump times to dt / 2^L."""
