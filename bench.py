@@ -200,14 +200,15 @@ def main():
         batch = SW.c3_rank_shard(rank, ws)
         protocol, n_steps, n_seg = "smooth_jp", 300, 300
         workload = ("C3: 100k-point (Omega, Omega*tau) smooth-JP Pareto sweep per GPU, 300 "
-                    "reference segments, medium apparatus, full reference noise model")
+                    "reference segments, medium apparatus, 4 collapse ops (sqrt(gamma_r)|1><r| and "
+                    "sqrt(gamma_phi) P_r per atom, gamma_r = 1/140 us, gamma_phi = 2pi x 10 kHz)")
     else:
         batch = SW.c4_rank_shard(rank, ws)
         protocol, n_steps, n_seg = "lp_square", None, 2
         workload = ("C4: 1M-point species {Rb87, Cs133} x T logspace(1-100 uK, 1000) x P_tweezer "
                     "logspace(1-100 mW, 500) LP-square grid, range-sharded over the ranks, "
                     "medium apparatus, full reference noise model")
-    params = E.pack_params(batch)
+    params = SW.c3_four_op_params(batch) if args.workload == "c3" else E.pack_params(batch)
     n = batch.n
     eng = E.Engine(devices=[local])
     db = E.DeviceBatch(eng, params, protocol, "lindblad", n_steps=n_steps, method=args.method)

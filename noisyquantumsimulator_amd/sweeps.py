@@ -82,6 +82,26 @@ def pareto_tgate_grid(n_omega: int = 1000, n_tau: int = 100, include_noise: bool
                            overrides=dict(laser_2_power=p2, omega_tau=OT.ravel()))
 
 
+# C3's noise model as BASELINE configs[2] / SURVEY.md §8d state it: 4 collapse ops,
+# sqrt(gamma_r)|1><r| and sqrt(gamma_phi) P_r on each atom
+C3_GAMMA_R = 1.0 / 140e-6               # 7142.857 s^-1 (Rb87 n = 70 Rydberg lifetime)
+C3_GAMMA_PHI = 2 * np.pi * 1e4
+
+
+def c3_four_op_params(batch: PH.DerivedBatch) -> np.ndarray:
+    """Packed parameters of a C3 batch with the 4-collapse-op model (Rydberg decay to
+    |1> + Rydberg dephasing on each atom) in place of the full reference noise."""
+    from . import engine as E
+    p = E.pack_params(batch)
+    P = E.N.P
+    for ab in ("A", "B"):
+        p[P["G1_" + ab]] = C3_GAMMA_R
+        p[P["G0_" + ab]] = 0.0
+        p[P["GPHI_" + ab]] = C3_GAMMA_PHI
+        p[P["GSC_" + ab]] = 0.0
+    return p
+
+
 C4_SHAPE = (2, 1000, 500)          # species x T x P_tweezer
 C4_POINTS = 2 * 1000 * 500
 

@@ -53,13 +53,18 @@ def main():
         b = SW.pareto_tgate_grid()
         idx = np.linspace(0, b.n - 1, a.sample).astype(int)
         c = b.cols
+        # the 4-collapse-op C3 model (sweeps.c3_four_op_params)
+        I3 = np.eye(3)
+        s1r, pr = O._trans(3, 1, 2), O._proj(3, 2)
+        c4 = [np.sqrt(SW.C3_GAMMA_R) * np.kron(s1r, I3), np.sqrt(SW.C3_GAMMA_R) * np.kron(I3, s1r),
+              np.sqrt(SW.C3_GAMMA_PHI) * np.kron(pr, I3), np.sqrt(SW.C3_GAMMA_PHI) * np.kron(I3, pr)]
         specs = [O.PointSpec(protocol="smooth_jp", Omega=c["Omega"][i], V=c["V"][i], Delta=c["Delta_seg"][i],
                              tau=c["tau_total"][i], A=c["A"][i], omega_mod=c["omega_mod"][i],
                              phi_offset=c["phi_offset"][i], n_steps=300, delta_zeeman=c["delta_zeeman"][i],
-                             delta_stark=c["delta_stark"][i],
-                             c_ops=O.collapse_operators({k: c[k][i] for k in O.RATE_KEYS}))
+                             delta_stark=c["delta_stark"][i], c_ops=c4)
                  for i in idx]
-        return _time(a, specs, "the C3 100k smooth-JP sweep (300 segments, ZVODE restarted per segment)")
+        return _time(a, specs, "the C3 100k smooth-JP sweep (300 segments, ZVODE restarted per segment, "
+                               "4 collapse ops)")
     if a.workload == "c2":
         b = SW.omega_delta_grid()
         idx = np.linspace(0, b.n - 1, a.sample).astype(int)

@@ -1,0 +1,51 @@
+"""C3 (BASELINE configs[2]): smooth-JP Pareto sweep points with the 4-collapse-op model
+(sqrt(gamma_r)|1><r| and sqrt(gamma_phi) P_r per atom), 300 reference segments, on the
+GPU against the expm oracle; plus the size-independent properties of a full-width
+shard (trace, positivity)."""
+import warnings
+
+import numpy as np
+import pytest
+
+from noisyquantumsimulator_amd import engine as E
+from noisyquantumsimulator_amd import sweeps as SW
+from oracle import lindblad_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _c_ops():
+    I3 = np.eye(3)
+    s1r, pr = O._trans(3, 1, 2), O._proj(3, 2)
+    g, f = np.sqrt(SW.C3_GAMMA_R), np.sqrt(SW.C3_GAMMA_PHI)
+    return [g * np.kron(s1r, I3), g * np.kron(I3, s1r), f * np.kron(pr, I3), f * np.kron(I3, pr)]
+
+
+def test_c3_four_op_points_match_oracle():
+    warnings.simplefilter("ignore")
+    b = SW.pareto_tgate_grid(n_omega=10, n_tau=10)
+    p = SW.c3_four_op_params(b)
+    eng = E.Engine()
+    r = eng.run(p, "smooth_jp", "lindblad", n_steps=300)
+    assert np.all(r.status == 0)
+    rho = r.rho()
+    c = b.cols
+    for i in (0, 37, 99):
+        spec = O.PointSpec(protocol="smooth_jp", Omega=c["Omega"][i], V=c["V"][i], Delta=c["Delta_seg"][i],
+                           tau=c["tau_total"][i], A=c["A"][i], omega_mod=c["omega_mod"][i],
+                           phi_offset=c["phi_offset"][i], n_steps=300, delta_zeeman=c["delta_zeeman"][i],
+                           delta_stark=c["delta_stark"][i], c_ops=_c_ops())
+        ref = O.run_point(spec)
+        for k, lab in enumerate(O.LABELS):
+            np.testing.assert_allclose(rho[i, k], ref[lab], atol=1e-10, rtol=0, err_msg=f"{i}/{lab}")
+
+
+def test_c3_shard_properties():
+    warnings.simplefilter("ignore")
+    b = SW.c3_rank_shard(0, 1, n_omega_per_rank=100)    # 10k points of the C3 layout
+    p = SW.c3_four_op_params(b)
+    r = E.Engine().run(p, "smooth_jp", "lindblad", n_steps=300)
+    assert np.all(r.status == 0)
+    rho = r.rho()
+    np.testing.assert_allclose(np.einsum("nkaa->nk", rho), 1.0, atol=1e-11)
+    assert np.linalg.eigvalsh(rho[::50]).min() > -1e-11
