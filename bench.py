@@ -35,7 +35,9 @@ FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (spec)
 # FLOPs per generator application (one 25-vector): apply_A 75 + apply_B 75 + V 12 + Clenshaw 25 FMAs
 FLOP_PER_MATVEC = 2 * (75 + 75 + 12 + 25)
 FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
-FLOP_PER_SQUARING_SYM = 2 * (15 ** 3 + 10 ** 3)   # identical atoms: sym (+) antisym blocks
+# identical atoms: only the block-triangular symmetric block [[B, C], [0, D]] (5 + 10):
+# B^2 (125) + BC + CD (250 + 500) + D^2 (1000) FMAs
+FLOP_PER_SQUARING_SYM = 2 * (5 ** 3 + 5 * 5 * 10 + 5 * 10 * 10 + 10 ** 3)
 FLOP_PER_STATE_UPDATE = 2 * 4 * 25 ** 2  # R_k <- U R_k for the 4 inputs, per segment
 N_OMEGA, N_DELTA = 100, 100
 # PMC-measured HBM bytes per launch of the dominant kernel (rocprofv3 --pmc FETCH_SIZE /

@@ -863,7 +863,7 @@ __host__ __device__ constexpr int asym_index(int i, int j) {     // i < j
   return i * 4 - i * (i - 1) / 2 + (j - i - 1);
 }
 constexpr double RSQRT2 = 0.70710678118654752440;
-constexpr int NS = 15, NA = 10;
+constexpr int NS = 15;                       // symmetric coordinates (the 10 antisymmetric are not built)
 
 // Build U = exp(L(g) g.dt) for every point of the block (block-uniform control
 // flow; lane (pl, j) computes one Chebyshev column, then one output tile per
@@ -912,7 +912,8 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
   double v[25];
 #pragma unroll
   for (int e = 0; e < 25; ++e) v[e] = (e == e1) ? w0 : ((e == e2) ? w2 : 0.0);
-  cheb_segment<25>(v, y, active,
+  // SYM: only the 15 symmetric columns are needed (see the squaring below)
+  cheb_segment<25>(v, y, active && (!SYM || is_sym),
                    [&](const double (&b)[25], double (&o)[25]) { apply_L<SYM>(A, B, vs, b, o); },
                    nuse, nexec);
   if (t == 0) s_max = 0;
@@ -929,30 +930,66 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
         for (int j2 = i2; j2 < 5; ++j2)
           Ub[sym_index(i2, j2) * NS + j] =
               (i2 == j2) ? v[5 * i2 + i2] : RSQRT2 * (v[5 * i2 + j2] + v[5 * j2 + i2]);
-    } else {                                // Ua[a'][j-15] = <asym_a', v>
-#pragma unroll
-      for (int i2 = 0; i2 < 5; ++i2)
-#pragma unroll
-        for (int j2 = i2 + 1; j2 < 5; ++j2)
-          Ub[NS * NS + asym_index(i2, j2) * NA + (j - NS)] = RSQRT2 * (v[5 * i2 + j2] - v[5 * j2 + i2]);
     }
+    // (SYM: the antisymmetric block is not built -- see the squaring below)
     atomicMax(&s_max, sq);
   }
   __syncthreads();
   const int smx = s_max;
   nsq += (double)sq;
-  // (2) squarings.  Full: lane owns the 5x5 tile (j/5, j%5) of U U.  SYM: lanes
-  // 0-14 own 5x3 tiles of Us (K = 15), lanes 15-24 own 5x2 tiles of Ua (K = 10),
-  // all with one code path (3 columns; a 5x2 tile repeats its last column).
-  const int ld = SYM ? (is_sym ? NS : NA) : NC;
+  // (2) squarings.  Full: lane owns the 5x5 tile (j/5, j%5) of U U.
+  // SYM: the symmetric block is block-triangular, Us = [[B, C], [0, D]] over the
+  // coordinates (0, m) (atom A or B in |0><0|: an invariant subspace, the single-atom
+  // propagator) and the other 10, so Us^2 = [[B^2, BC + CD], [0, D^2]]: 1875 FMAs,
+  // 75 per lane (one B^2 entry, a 1x2 tile of BC + CD, a 2x2 tile of D^2).  The
+  // antisymmetric block is never needed: the 4 basis inputs have antisymmetric
+  // parts only on the (0, m) coordinates, where the propagator is B again.
+  if (SYM) {
+    const int rb = j / 5, cb = j % 5;
+    const int cc = 5 + 2 * cb, rd = 5 + 2 * rb;
+    for (int it = 0; it < smx; ++it) {
+      double b2 = 0.0, c2a = 0.0, c2b = 0.0, d00 = 0.0, d01 = 0.0, d10 = 0.0, d11 = 0.0;
+      const bool go = lane_ok && it < sq;
+      if (go) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) b2 = fma(Ub[rb * NS + k], Ub[k * NS + cb], b2);
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+          const double a = Ub[rb * NS + k];
+          c2a = fma(a, Ub[k * NS + cc], c2a);
+          c2b = fma(a, Ub[k * NS + cc + 1], c2b);
+        }
+#pragma unroll
+        for (int k = 5; k < NS; ++k) {
+          const double a0 = Ub[rd * NS + k], a1 = Ub[(rd + 1) * NS + k];
+          const double e0 = Ub[k * NS + cc], e1 = Ub[k * NS + cc + 1];
+          d00 = fma(a0, e0, d00);
+          d01 = fma(a0, e1, d01);
+          d10 = fma(a1, e0, d10);
+          d11 = fma(a1, e1, d11);
+        }
+      }
+      __syncthreads();
+      if (go) {
+        Ub[rb * NS + cb] = b2;
+        Ub[rb * NS + cc] = c2a;
+        Ub[rb * NS + cc + 1] = c2b;
+        Ub[rd * NS + cc] = d00;
+        Ub[rd * NS + cc + 1] = d01;
+        Ub[(rd + 1) * NS + cc] = d10;
+        Ub[(rd + 1) * NS + cc + 1] = d11;
+      }
+      __syncthreads();
+    }
+  }
+  const int ld = NC;
   const int nk = ld;
-  const int boff = SYM ? (is_sym ? 0 : NS * NS) : 0;
-  const int r0 = SYM ? (is_sym ? 5 * (j / 5) : 5 * ((j - NS) / 5)) : 5 * (j / 5);
-  const int c0 = SYM ? (is_sym ? 3 * (j % 5) : 2 * ((j - NS) % 5)) : 5 * (j % 5);
-  const int ncol = SYM ? (is_sym ? 3 : 2) : 5;
-  constexpr int TC = SYM ? 3 : 5;           // tile columns held per lane
-  const double* Mb = Ub + boff;
-  for (int it = 0; it < smx; ++it) {
+  const int r0 = 5 * (j / 5);
+  const int c0 = 5 * (j % 5);
+  const int ncol = 5;
+  constexpr int TC = 5;                     // tile columns held per lane
+  const double* Mb = Ub;
+  for (int it = 0; it < (SYM ? 0 : smx); ++it) {
     double acc[5][TC];
 #pragma unroll
     for (int a = 0; a < 5; ++a)
@@ -976,7 +1013,7 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
     }
     __syncthreads();
     if (lane_ok && it < sq) {
-      double* Mw = Ub + boff;
+      double* Mw = Ub;
 #pragma unroll
       for (int a = 0; a < 5; ++a)
 #pragma unroll
@@ -997,7 +1034,7 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
     const int ar_ = (ra == rb) ? 0 : asym_index(lo, hi);
     const double war = (ra == rb) ? 0.0 : (ra < rb ? RSQRT2 : -RSQRT2);
     const double* Us = Ub;
-    const double* Ua = Ub + NS * NS;
+    (void)ar_;
 #pragma unroll
     for (int m = 0; m < NC; ++m) {
       const int ca = m / 5, cb = m % 5;
@@ -1005,7 +1042,10 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
       const double wsc = (ca == cb) ? 1.0 : RSQRT2;
       const double wac = (ca == cb) ? 0.0 : (ca < cb ? RSQRT2 : -RSQRT2);
       double val = wsr * wsc * Us[sr * NS + sym_index(clo, chi)];
-      if (ca != cb) val = fma(war * wac, Ua[ar_ * NA + asym_index(clo, chi)], val);
+      // antisymmetric part: on the (0, m) coordinates it is the single-atom block B
+      // (Ua[(0,hi)][(0,chi)] = Us[(0,hi)][(0,chi)] = Us[hi][chi]); elsewhere the basis
+      // inputs never have support, so it is left out
+      if (ca != cb && lo == 0 && clo == 0) val = fma(war * wac, Us[hi * NS + chi], val);
       u[m] = val;
     }
   }
@@ -1171,7 +1211,7 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
     sm[(int64_t)RYD_S_CTRL_PHASE * ldm + i] = nan;
     sm[(int64_t)RYD_S_PENALTY * ldm + i] = nan;
     sm[(int64_t)RYD_S_AVG_F * ldm + i] = avg;
-    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = NC * nuse;   // 25 basis columns per point
+    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = (SYM ? NS : NC) * nuse;   // basis columns per point
     sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = NC * nexec;
     sm[(int64_t)RYD_S_TRACE11 * ldm + i] = tr11;
     sm[(int64_t)RYD_S_NSQUARE * ldm + i] = nsq;
