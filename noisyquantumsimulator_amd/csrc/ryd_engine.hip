@@ -826,12 +826,13 @@ __global__ __launch_bounds__(BLOCK) void lindblad4_cheb_kernel(
 constexpr int PPB = 10;                     // points per 256-lane block (250 lanes used)
 constexpr int NC = 25;
 // Chebyshev argument after scaling.  Lower means fewer Chebyshev terms and more
-// squarings: with the cheap exchange-symmetric squaring (4375 FMAs) 2 is best, with
-// the full 25^3 one 3-6 are equal (profiles/r01/tune_*).  RYD_X_BASE overrides both.
+// squarings: with the block-triangular symmetric squaring (1875 FMAs, 75 per lane)
+// 0.5 is best (C2 0.093 ms vs 0.098 at 2; C3 flat), with the full 25^3 one 3-6 are
+// equal (profiles/r01/tune_*).  RYD_X_BASE overrides both.
 #ifdef RYD_X_BASE
 constexpr double X_BASE_SYM = RYD_X_BASE, X_BASE_FULL = RYD_X_BASE;
 #else
-constexpr double X_BASE_SYM = 2.0, X_BASE_FULL = 6.0;
+constexpr double X_BASE_SYM = 0.5, X_BASE_FULL = 6.0;
 #endif
 
 template <int PROTO>
