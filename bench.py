@@ -38,7 +38,9 @@ FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
 # identical atoms: only the block-triangular symmetric block [[B, C], [0, D]] (5 + 10):
 # B^2 (125) + BC + CD (250 + 500) + D^2 (1000) FMAs
 FLOP_PER_SQUARING_SYM = 2 * (5 ** 3 + 5 * 5 * 10 + 5 * 10 * 10 + 10 ** 3)
-FLOP_PER_STATE_UPDATE = 2 * 4 * 25 ** 2  # R_k <- U R_k for the 4 inputs, per segment
+# R_k <- U R_k for the 4 inputs per segment, each over its support (|00>: 1, |01>/|10>: 5,
+# |11>: 25 coordinates), 25 rows
+FLOP_PER_STATE_UPDATE = 2 * 25 * (1 + 5 + 5 + 25)
 N_OMEGA, N_DELTA = 100, 100
 # PMC-measured HBM bytes per launch of the dominant kernel (rocprofv3 --pmc FETCH_SIZE /
 # WRITE_SIZE in separate passes, FETCH_SIZE x2 per MI355X_MICROARCH.md), committed under

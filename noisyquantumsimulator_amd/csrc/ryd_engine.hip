@@ -1052,6 +1052,45 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
   }
 }
 
+// Row j of U applied to the 4 basis-input states, each summed over its support only:
+// |00>: coordinate 0 (e00 (x) e00); |01>: atom A in |0><0| (coordinates 0..4); |10>:
+// atom B in |0><0| (0, 5, .., 20); |11>: all 25.  A subspace with an atom in |0><0| is
+// invariant (that atom's column of M is zero and V needs both atoms in r), so the
+// skipped terms are exact zeros and the sums are bit-identical to the full ones.
+__device__ __forceinline__ void update_rows(const double (&u)[NC], const double (&R)[4][NC], double (&nr)[4]) {
+  nr[0] = fma(u[0], R[0][0], 0.0);
+  nr[1] = nr[2] = nr[3] = 0.0;
+#pragma unroll
+  for (int m = 0; m < 5; ++m) nr[1] = fma(u[m], R[1][m], nr[1]);
+#pragma unroll
+  for (int a = 0; a < 5; ++a) nr[2] = fma(u[5 * a], R[2][5 * a], nr[2]);
+#pragma unroll
+  for (int m = 0; m < NC; ++m) nr[3] = fma(u[m], R[3][m], nr[3]);
+}
+
+// o = (Q1 (x) Q1)^T u for a propagator row u, so that o . R = u . (Q R): the frame
+// rotation of rotate_coord moved onto the lane's own row (registers only).  Q1 mixes
+// the (ex, ey) coordinates 3, 4: rows [c s; -s c].
+__device__ __forceinline__ void rot_row(const double (&u)[NC], double c, double s, double (&o)[NC]) {
+  double t[NC];
+#pragma unroll
+  for (int b = 0; b < 5; ++b) {
+    t[b] = u[b];
+    t[5 + b] = u[5 + b];
+    t[10 + b] = u[10 + b];
+    t[15 + b] = fma(c, u[15 + b], -s * u[20 + b]);
+    t[20 + b] = fma(s, u[15 + b], c * u[20 + b]);
+  }
+#pragma unroll
+  for (int a = 0; a < 5; ++a) {
+    o[5 * a] = t[5 * a];
+    o[5 * a + 1] = t[5 * a + 1];
+    o[5 * a + 2] = t[5 * a + 2];
+    o[5 * a + 3] = fma(c, t[5 * a + 3], -s * t[5 * a + 4]);
+    o[5 * a + 4] = fma(s, t[5 * a + 3], c * t[5 * a + 4]);
+  }
+}
+
 // dst_k[j] = (Q(c,s) R_k)[j] for this lane's coordinate j = 5a + b, Q = Q1 (x) Q1:
 // coordinate 3 -> c r3 + s r4, coordinate 4 -> -s r3 + c r4 on each atom index.
 __device__ __forceinline__ void rotate_coord(const double (&src)[4][NC], double (&dst)[4][NC], int j,
@@ -1123,13 +1162,7 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
     if (!use_frame) {
       // R_k <- U R_k ; lane (pl, r = j) computes row r for the 4 inputs
       double nr[4] = {0.0, 0.0, 0.0, 0.0};
-      if (lane_ok) {
-#pragma unroll
-        for (int m = 0; m < NC; ++m) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) nr[k] = fma(u[m], Rs[pl][k][m], nr[k]);
-        }
-      }
+      if (lane_ok) update_rows(u, Rs[pl], nr);
       __syncthreads();
       if (lane_ok) {
 #pragma unroll
@@ -1148,28 +1181,34 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
       const PointP q = load_point<PROTO>(pp, ldp, i);
       double c, sn;
       segment_phase<PROTO>(q, s, n_steps, c, sn);
-      // into this segment's frame: Q_s^T Q_{s-1} = Q(phi_{s-1} - phi_s)
+      // into this segment's frame, Q_s^T Q_{s-1} = Q(phi_{s-1} - phi_s), folded into
+      // the lane's row; the states ping-pong between Rs and Rt (one barrier a segment)
       const double cr = cp * c + sp * sn, sr = sp * c - cp * sn;
-      if (lane_ok) rotate_coord(Rs[pl], Rt[pl], j, cr, sr);
-      __syncthreads();
-      double nr[4] = {0.0, 0.0, 0.0, 0.0};
       if (lane_ok) {
+        double ur[NC], nr[4];
+        rot_row(u, cr, sr, ur);
+        if ((s & 1) == 0) {
+          update_rows(ur, Rs[pl], nr);
 #pragma unroll
-        for (int m = 0; m < NC; ++m) {
+          for (int k = 0; k < 4; ++k) Rt[pl][k][j] = nr[k];
+        } else {
+          update_rows(ur, Rt[pl], nr);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) nr[k] = fma(u[m], Rt[pl][k][m], nr[k]);
+          for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
       }
       __syncthreads();
       cp = c;
       sp = sn;
     }
-    // back to the lab frame: Q_{N-1}
-    if (lane_ok) rotate_coord(Rs[pl], Rt[pl], j, cp, sp);
-    __syncthreads();
+    // back to the lab frame: Q_{N-1}; the result ends in Rs
+    const bool in_t = (nseg & 1) != 0;       // the latest state is in Rt
     if (lane_ok) {
+      if (in_t) rotate_coord(Rt[pl], Rs[pl], j, cp, sp);
+      else rotate_coord(Rs[pl], Rt[pl], j, cp, sp);
+    }
+    __syncthreads();
+    if (!in_t && lane_ok) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) Rs[pl][k][j] = Rt[pl][k][j];
     }
