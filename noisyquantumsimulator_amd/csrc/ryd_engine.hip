@@ -1175,12 +1175,39 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
   if (use_frame) {
     // U0 row j stays in registers for every segment
     double cp = 1.0, sp = 0.0;               // phase of the frame R is currently in
+    // Smooth JP: the (cos, sin) of every segment's phase (a cos and a sincos in fp64)
+    // is computed once per (point, segment) by the whole block into a table that
+    // reuses U's LDS (free now: each lane holds its row) instead of redundantly by
+    // the point's 25 lanes every segment; same arithmetic, so the same bits.
+    constexpr bool TAB = PROTO == RYD_PROTO_SMOOTH_JP;
+    constexpr int CH = (NC * NC) / 2;        // segments per table chunk (312)
+    static_assert(2 * CH <= NC * NC, "phase table must fit in U");
+    double* ph = &U[0][0][0];                // ph[(p * CH + s % CH) * 2 + {0: cos, 1: sin}]
     for (int s = 0; s < nseg; ++s) {
-      const double* pp = prm;
-      asm volatile("" : "+s"(pp));
-      const PointP q = load_point<PROTO>(pp, ldp, i);
       double c, sn;
-      segment_phase<PROTO>(q, s, n_steps, c, sn);
+      if (TAB) {
+        if (s % CH == 0) {
+          const int len = nseg - s < CH ? nseg - s : CH;
+          __syncthreads();                   // U rows / the previous chunk fully read
+          for (int e = t; e < PPB * len; e += BLOCK) {
+            const int p = e / len, sl = e % len;
+            const int64_t ie = (int64_t)blockIdx.x * PPB + p;
+            const PointP qe = load_point<PROTO>(prm, ldp, ie < n ? ie : n - 1);
+            double ce, se;
+            segment_phase<PROTO>(qe, s + sl, n_steps, ce, se);
+            ph[(p * CH + sl) * 2] = ce;
+            ph[(p * CH + sl) * 2 + 1] = se;
+          }
+          __syncthreads();
+        }
+        c = ph[(pl * CH + s % CH) * 2];
+        sn = ph[(pl * CH + s % CH) * 2 + 1];
+      } else {
+        const double* pp = prm;
+        asm volatile("" : "+s"(pp));
+        const PointP q = load_point<PROTO>(pp, ldp, i);
+        segment_phase<PROTO>(q, s, n_steps, c, sn);
+      }
       // into this segment's frame, Q_s^T Q_{s-1} = Q(phi_{s-1} - phi_s), folded into
       // the lane's row; the states ping-pong between Rs and Rt (one barrier a segment)
       const double cr = cp * c + sp * sn, sr = sp * c - cp * sn;
