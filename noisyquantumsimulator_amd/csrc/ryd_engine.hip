@@ -1091,6 +1091,35 @@ __device__ __forceinline__ void rot_row(const double (&u)[NC], double c, double 
   }
 }
 
+// update_rows(rot_row(u, c, s), R): the rotated row produced one atom-A index a at a
+// time and consumed at once (ascending coordinate order, the same expressions), so
+// the 25 rotated coefficients are never live together -- same bits, fewer VGPRs.
+__device__ __forceinline__ void update_rows_rot(const double (&u)[NC], double c, double s,
+                                                const double (&R)[4][NC], double (&nr)[4]) {
+  nr[0] = nr[1] = nr[2] = nr[3] = 0.0;
+#pragma unroll
+  for (int a = 0; a < 5; ++a) {
+    double t[5], o[5];
+#pragma unroll
+    for (int b = 0; b < 5; ++b)
+      t[b] = a < 3 ? u[5 * a + b]
+                   : (a == 3 ? fma(c, u[15 + b], -s * u[20 + b]) : fma(s, u[15 + b], c * u[20 + b]));
+    o[0] = t[0];
+    o[1] = t[1];
+    o[2] = t[2];
+    o[3] = fma(c, t[3], -s * t[4]);
+    o[4] = fma(s, t[3], c * t[4]);
+    if (a == 0) {
+      nr[0] = fma(o[0], R[0][0], 0.0);
+#pragma unroll
+      for (int b = 0; b < 5; ++b) nr[1] = fma(o[b], R[1][b], nr[1]);
+    }
+    nr[2] = fma(o[0], R[2][5 * a], nr[2]);
+#pragma unroll
+    for (int b = 0; b < 5; ++b) nr[3] = fma(o[b], R[3][5 * a + b], nr[3]);
+  }
+}
+
 // dst_k[j] = (Q(c,s) R_k)[j] for this lane's coordinate j = 5a + b, Q = Q1 (x) Q1:
 // coordinate 3 -> c r3 + s r4, coordinate 4 -> -s r3 + c r4 on each atom index.
 __device__ __forceinline__ void rotate_coord(const double (&src)[4][NC], double (&dst)[4][NC], int j,
@@ -1282,6 +1311,177 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
     sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = NC * nexec;
     sm[(int64_t)RYD_S_TRACE11 * ldm + i] = tr11;
     sm[(int64_t)RYD_S_NSQUARE * ldm + i] = nsq;
+    status[i] = stat;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Smooth JP in two launches (many segments, one propagator)
+// ---------------------------------------------------------------------------
+// The fused kernel above runs smooth JP's 300 frame-rotated state updates at the
+// occupancy its propagator build needs (255 VGPRs, 66 KB LDS: 2 waves per SIMD) and
+// with a block barrier per segment, because its 25-lane points straddle waves.
+// Split: jp_rows_kernel builds the phase-0 propagator (build_propagator, as above)
+// and writes each lane's row to a workspace; jp_frame_kernel walks the segments with
+// two points per wave (32 lanes each, 25 used), so every exchange is wave-local (no
+// s_barrier), ~100 VGPRs and 21 KB LDS per block (several blocks per CU hide the
+// LDS latency).  Same operands and operation order as the fused path: same bits.
+constexpr int FPW = 2;                       // points per wave (frame kernel)
+constexpr int FPB = FPW * (BLOCK / 64);      // 8 points per block
+constexpr int FCH = 64;                      // segments per wave-local phase-table chunk
+
+// LDS exchange among the lanes of one wave: a wave's LDS operations complete in
+// order, so ordering the compiler is all that is needed (no s_barrier).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// W[m][25 i + j] = row j, column m of point i's phase-0 segment propagator
+template <bool SYM>
+__global__ __launch_bounds__(BLOCK, 2) void jp_rows_kernel(
+    const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ W,
+    double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
+  constexpr int PROTO = RYD_PROTO_SMOOTH_JP;
+  __shared__ __attribute__((aligned(16))) double U[PPB][NC][NC];
+  __shared__ int s_max;
+  const int t = threadIdx.x;
+  const bool lane_ok = t < PPB * NC;
+  const int pl = lane_ok ? t / NC : 0;
+  const int j = t % NC;
+  const int64_t ip = (int64_t)blockIdx.x * PPB + pl;
+  const bool live = lane_ok && ip < n;
+  const int64_t i = ip < n ? ip : n - 1;
+  const PointP q = load_point<PROTO>(prm, ldp, i);
+  const bool valid = point_valid<PROTO>(q, n_steps);
+  double nuse = 0.0, nexec = 0.0, nsq = 0.0;
+  bool over_cap = false;
+  Seg g = segment<PROTO>(q, 0, n_steps, shape);
+  g.om_re = q.Om;                            // reference frame: phase 0
+  g.om_im = 0.0;
+  double u[NC];
+  build_propagator<SYM>(U, s_max, q, g, valid, lane_ok, t, pl, j, nuse, nexec, nsq, over_cap, u);
+  if (live) {
+    const int64_t ld = (int64_t)NC * n;
+#pragma unroll
+    for (int m = 0; m < NC; ++m) W[m * ld + NC * i + j] = u[m];
+  }
+  if (live && j == 0) {
+    uint32_t stat = valid ? 0u : RYD_STATUS_BAD_INPUT;
+    if (over_cap) stat |= RYD_STATUS_STEP_CAP;
+    status[i] = stat;
+    sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = (SYM ? NS : NC) * nuse;
+    sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = NC * nexec;
+    sm[(int64_t)RYD_S_NSQUARE * ldm + i] = nsq;
+  }
+}
+
+template <int OCC>                           // waves per SIMD the register budget targets
+__global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
+    const double* __restrict__ prm, int64_t n, int64_t ldp, const double* __restrict__ W,
+    double* __restrict__ st, int64_t lds, double* __restrict__ sm, int64_t ldm,
+    uint32_t* __restrict__ status, int n_steps) {
+  constexpr int PROTO = RYD_PROTO_SMOOTH_JP;
+  __shared__ __attribute__((aligned(16))) double Rs[FPB][4][NC];
+  __shared__ __attribute__((aligned(16))) double Rt[FPB][4][NC];
+  __shared__ __attribute__((aligned(16))) double ph[FPB][FCH][2];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  const int j = l & 31;
+  const int pl = FPW * w + (l >> 5);
+  const bool lane_ok = j < NC;
+  const int jj = lane_ok ? j : 0;
+  const int64_t ip = (int64_t)blockIdx.x * FPB + pl;
+  const bool live = lane_ok && ip < n;
+  const int64_t i = ip < n ? ip : n - 1;
+  double u[NC];
+  {
+    const int64_t ld = (int64_t)NC * n;
+#pragma unroll
+    for (int m = 0; m < NC; ++m) u[m] = W[m * ld + NC * i + jj];
+  }
+  for (int e = l; e < FPW * 4 * NC; e += 64) {
+    const int p = FPW * w + e / (4 * NC), k = (e / NC) % 4, r = e % NC;
+    const int e0 = 5 * (k >> 1) + (k & 1);
+    Rs[p][k][r] = (r == e0) ? 1.0 : 0.0;
+  }
+  wave_sync();
+  const int nseg = n_segments<PROTO>(n_steps);
+  double cp = 1.0, sp = 0.0;                 // phase of the frame R is currently in
+  for (int s = 0; s < nseg; ++s) {
+    if (s % FCH == 0) {                      // this wave's two points, next FCH segments
+      const int len = nseg - s < FCH ? nseg - s : FCH;
+      for (int e = l; e < FPW * len; e += 64) {
+        const int p = e / len, sl = e % len;
+        const int64_t ie = (int64_t)blockIdx.x * FPB + FPW * w + p;
+        const PointP qe = load_point<PROTO>(prm, ldp, ie < n ? ie : n - 1);
+        double ce, se;
+        segment_phase<PROTO>(qe, s + sl, n_steps, ce, se);
+        ph[FPW * w + p][sl][0] = ce;
+        ph[FPW * w + p][sl][1] = se;
+      }
+      wave_sync();
+    }
+    const double c = ph[pl][s % FCH][0], sn = ph[pl][s % FCH][1];
+    const double cr = cp * c + sp * sn, sr = sp * c - cp * sn;
+    if (lane_ok) {
+      double nr[4];
+      if ((s & 1) == 0) {
+        update_rows_rot(u, cr, sr, Rs[pl], nr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) Rt[pl][k][j] = nr[k];
+      } else {
+        update_rows_rot(u, cr, sr, Rt[pl], nr);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
+      }
+    }
+    wave_sync();
+    cp = c;
+    sp = sn;
+  }
+  // back to the lab frame: Q_{N-1}; the result ends in Rs
+  const bool in_t = (nseg & 1) != 0;
+  if (lane_ok) {
+    if (in_t) rotate_coord(Rt[pl], Rs[pl], j, cp, sp);
+    else rotate_coord(Rs[pl], Rt[pl], j, cp, sp);
+  }
+  wave_sync();
+  if (!in_t && lane_ok) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Rs[pl][k][j] = Rt[pl][k][j];
+  }
+  wave_sync();
+  if (live) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[(int64_t)j * lds + 4 * i + k] = Rs[pl][k][j];
+  }
+  if (live && j == 0) {
+    uint32_t stat = status[i];               // BAD_INPUT / STEP_CAP from jp_rows_kernel
+    double pops[4], tr11 = 0.0;
+    bool fin = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pops[k] = Rs[pl][k][5 * (k >> 1) + (k & 1)];
+    for (int r = 0; r < NC; ++r)
+      for (int k = 0; k < 4; ++k) fin = fin && isfinite(Rs[pl][k][r]);
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) tr11 += Rs[pl][3][5 * a + b];
+    if (!fin) stat |= RYD_STATUS_NONFINITE;
+    const double nan = __builtin_nan("");
+    const double avg = 0.25 * (pops[0] + pops[1] + pops[2] + pops[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sm[(int64_t)(RYD_S_POP0 + k) * ldm + i] = pops[k];
+      sm[(int64_t)(RYD_S_OV_RE0 + k) * ldm + i] = nan;
+      sm[(int64_t)(RYD_S_OV_IM0 + k) * ldm + i] = nan;
+    }
+    sm[(int64_t)RYD_S_AVG_POP * ldm + i] = avg;
+    sm[(int64_t)RYD_S_CTRL_PHASE * ldm + i] = nan;
+    sm[(int64_t)RYD_S_PENALTY * ldm + i] = nan;
+    sm[(int64_t)RYD_S_AVG_F * ldm + i] = avg;
+    sm[(int64_t)RYD_S_TRACE11 * ldm + i] = tr11;
     status[i] = stat;
   }
 }
@@ -1810,6 +2010,49 @@ int validate(const ryd_batch_desc* d, int64_t n, int64_t ldp, int64_t lds, int64
   return RYD_OK;
 }
 
+// RYD_JP_SPLIT=0 keeps smooth JP in the fused lindblad_prop_kernel (A/B measurements)
+bool jp_split_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RYD_JP_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Smooth JP, propagator method: jp_rows_kernel -> workspace (25 x 25 doubles per
+// point, stream-ordered allocation, pool kept warm) -> jp_frame_kernel.
+int launch_jp_split(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, double* ds,
+                    int64_t lds, double* dm, int64_t ldm, uint32_t* dstat, hipStream_t stream) {
+  const bool sym = (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0;
+  const int64_t blocks_a = (n + PPB - 1) / PPB, blocks_b = (n + FPB - 1) / FPB;
+  if (blocks_b > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
+  {
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    hipMemPool_t pool;
+    HIPCHK(hipDeviceGetDefaultMemPool(&pool, dev));
+    uint64_t keep = UINT64_MAX;
+    HIPCHK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
+  }
+  double* W = nullptr;
+  HIPCHK(hipMallocAsync((void**)&W, sizeof(double) * NC * NC * (size_t)n, stream));
+  int ns = d->n_steps, sh = d->shape;
+  void* args_a[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&W, (void*)&dm, (void*)&ldm,
+                    (void*)&dstat, (void*)&ns, (void*)&sh};
+  const void* ka = sym ? (const void*)jp_rows_kernel<true> : (const void*)jp_rows_kernel<false>;
+  HIPCHK(hipLaunchKernel(ka, dim3((unsigned)blocks_a), dim3(BLOCK), args_a, 0, stream));
+  void* args_b[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&W, (void*)&ds, (void*)&lds,
+                    (void*)&dm, (void*)&ldm, (void*)&dstat, (void*)&ns};
+  static const int occ = [] {
+    const char* e = getenv("RYD_JP_OCC");
+    return (e && e[0] == '3') ? 3 : 4;
+  }();
+  const void* kb = occ == 3 ? (const void*)jp_frame_kernel<3> : (const void*)jp_frame_kernel<4>;
+  HIPCHK(hipLaunchKernel(kb, dim3((unsigned)blocks_b), dim3(BLOCK), args_b, 0, stream));
+  HIPCHK(hipFreeAsync(W, stream));
+  return RYD_OK;
+}
+
 int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, double* ds, int64_t lds,
            double* dm, int64_t ldm, uint32_t* dstat, hipStream_t stream) {
   if (n == 0) return RYD_OK;
@@ -1833,6 +2076,8 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
     HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(DP_BLOCK), args, 0, stream));
     return RYD_OK;
   }
+  if (use_propagator(d) && d->protocol == RYD_PROTO_SMOOTH_JP && jp_split_enabled())
+    return launch_jp_split(d, dp, n, ldp, ds, lds, dm, ldm, dstat, stream);
   KernelFn k = pick_kernel(d);
   if (!k) return fail(RYD_ERR_UNSUPPORTED, "no kernel for this descriptor");
   const int64_t blocks = use_propagator(d) ? (n + PPB - 1) / PPB : (4 * n + BLOCK - 1) / BLOCK;
