@@ -38,9 +38,10 @@ FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
 # identical atoms: only the block-triangular symmetric block [[B, C], [0, D]] (5 + 10):
 # B^2 (125) + BC + CD (250 + 500) + D^2 (1000) FMAs
 FLOP_PER_SQUARING_SYM = 2 * (5 ** 3 + 5 * 5 * 10 + 5 * 10 * 10 + 10 ** 3)
-# R_k <- U R_k for the 4 inputs per segment, each over its support (|00>: 1, |01>/|10>: 5,
-# |11>: 25 coordinates), 25 rows
-FLOP_PER_STATE_UPDATE = 2 * 25 * (1 + 5 + 5 + 25)
+# R_k <- U R_k for the 4 inputs per segment, each on its invariant support only (|00>: 1x1,
+# |01>/|10>: 5x5, |11>: 25x25); identical atoms: |10> is the atom-swap mirror of |01>
+FLOP_PER_STATE_UPDATE = 2 * (1 + 25 + 25 + 625)
+FLOP_PER_STATE_UPDATE_SYM = 2 * (1 + 25 + 625)
 N_OMEGA, N_DELTA = 100, 100
 # PMC-measured HBM bytes per launch of the dominant kernel (rocprofv3 --pmc FETCH_SIZE /
 # WRITE_SIZE in separate passes, FETCH_SIZE x2 per MI355X_MICROARCH.md), committed under
@@ -244,7 +245,8 @@ def main():
     sq_flops = FLOP_PER_SQUARING_SYM if E.symmetric_atoms(params) else FLOP_PER_SQUARING
     flops = res.matvec_useful * FLOP_PER_MATVEC + nsq * sq_flops
     if prop_kernel:
-        flops += n_seg * n * FLOP_PER_STATE_UPDATE       # R <- U R once per reference segment
+        upd = FLOP_PER_STATE_UPDATE_SYM if E.symmetric_atoms(params) else FLOP_PER_STATE_UPDATE
+        flops += n_seg * n * upd                         # R <- U R once per reference segment
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     tr = _measured_traffic(args.workload, args.method, n)
     traffic = tr["bytes_per_launch"] if tr else None

@@ -1120,6 +1120,27 @@ __device__ __forceinline__ void update_rows_rot(const double (&u)[NC], double c,
   }
 }
 
+// One basis input only: sum_m o[m] R[m] with o = rot_row(u, c, s) (the nr[3] chain of
+// update_rows_rot; with u zero outside an input's support the extra terms are exact zeros).
+__device__ __forceinline__ double update_row_rot(const double (&u)[NC], double c, double s,
+                                                 const double* __restrict__ R) {
+  double acc = 0.0;
+#pragma unroll
+  for (int a = 0; a < 5; ++a) {
+    double t[5];
+#pragma unroll
+    for (int b = 0; b < 5; ++b)
+      t[b] = a < 3 ? u[5 * a + b]
+                   : (a == 3 ? fma(c, u[15 + b], -s * u[20 + b]) : fma(s, u[15 + b], c * u[20 + b]));
+    acc = fma(t[0], R[5 * a], acc);
+    acc = fma(t[1], R[5 * a + 1], acc);
+    acc = fma(t[2], R[5 * a + 2], acc);
+    acc = fma(fma(c, t[3], -s * t[4]), R[5 * a + 3], acc);
+    acc = fma(fma(s, t[3], c * t[4]), R[5 * a + 4], acc);
+  }
+  return acc;
+}
+
 // dst_k[j] = (Q(c,s) R_k)[j] for this lane's coordinate j = 5a + b, Q = Q1 (x) Q1:
 // coordinate 3 -> c r3 + s r4, coordinate 4 -> -s r3 + c r4 on each atom index.
 __device__ __forceinline__ void rotate_coord(const double (&src)[4][NC], double (&dst)[4][NC], int j,
@@ -1377,7 +1398,13 @@ __global__ __launch_bounds__(BLOCK, 2) void jp_rows_kernel(
   }
 }
 
-template <int OCC>                           // waves per SIMD the register budget targets
+// Identical atoms (SYM): each 32-lane half is one point with one output per lane --
+// lanes 0..24 |11><11| row j (reads R_11), 25..29 |01><01| row j-25 (reads R_01, row
+// zeroed outside (0, m)), 30 |00><00| (row 0, column 0) -- 25 products a lane instead
+// of 36.  |10><10| is the atom-swap mirror of |01><01|, bit for bit (U[5a][5b] and
+// U[a][b] come from the same symmetric-block expression, the row rotation acts on the
+// same index pair), so lane 25 + r writes it too.
+template <int OCC, bool SYM>                 // OCC: waves per SIMD the register budget targets
 __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, const double* __restrict__ W,
     double* __restrict__ st, int64_t lds, double* __restrict__ sm, int64_t ldm,
@@ -1390,20 +1417,24 @@ __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
   const int j = l & 31;
   const int pl = FPW * w + (l >> 5);
   const bool lane_ok = j < NC;
-  const int jj = lane_ok ? j : 0;
+  const bool role_ok = SYM ? j < 31 : lane_ok;   // lanes that own an update output
+  const int row = j < NC ? j : (j < 30 ? j - NC : 0);
+  const int ksrc = j < NC ? 3 : (j < 30 ? 1 : 0);
   const int64_t ip = (int64_t)blockIdx.x * FPB + pl;
   const bool live = lane_ok && ip < n;
   const int64_t i = ip < n ? ip : n - 1;
   double u[NC];
   {
     const int64_t ld = (int64_t)NC * n;
+    const int mmax = (!SYM || j < NC) ? NC : (j < 30 ? 5 : (j == 30 ? 1 : 0));
 #pragma unroll
-    for (int m = 0; m < NC; ++m) u[m] = W[m * ld + NC * i + jj];
+    for (int m = 0; m < NC; ++m) u[m] = m < mmax ? W[m * ld + NC * i + row] : 0.0;
   }
   for (int e = l; e < FPW * 4 * NC; e += 64) {
     const int p = FPW * w + e / (4 * NC), k = (e / NC) % 4, r = e % NC;
     const int e0 = 5 * (k >> 1) + (k & 1);
     Rs[p][k][r] = (r == e0) ? 1.0 : 0.0;
+    Rt[p][k][r] = 0.0;                       // coordinates outside a support stay zero
   }
   wave_sync();
   const int nseg = n_segments<PROTO>(n_steps);
@@ -1424,16 +1455,24 @@ __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
     }
     const double c = ph[pl][s % FCH][0], sn = ph[pl][s % FCH][1];
     const double cr = cp * c + sp * sn, sr = sp * c - cp * sn;
-    if (lane_ok) {
-      double nr[4];
-      if ((s & 1) == 0) {
-        update_rows_rot(u, cr, sr, Rs[pl], nr);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) Rt[pl][k][j] = nr[k];
+    if (role_ok) {
+      double (&Rsrc)[4][NC] = (s & 1) == 0 ? Rs[pl] : Rt[pl];
+      double (&Rdst)[4][NC] = (s & 1) == 0 ? Rt[pl] : Rs[pl];
+      if (SYM) {
+        const double v = update_row_rot(u, cr, sr, Rsrc[ksrc]);
+        if (j < NC) {
+          Rdst[3][j] = v;
+        } else if (j < 30) {
+          Rdst[1][row] = v;
+          Rdst[2][5 * row] = v;
+        } else {
+          Rdst[0][0] = v;
+        }
       } else {
-        update_rows_rot(u, cr, sr, Rt[pl], nr);
+        double nr[4];
+        update_rows_rot(u, cr, sr, Rsrc, nr);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
+        for (int k = 0; k < 4; ++k) Rdst[k][j] = nr[k];
       }
     }
     wave_sync();
@@ -2043,11 +2082,8 @@ int launch_jp_split(const ryd_batch_desc* d, const double* dp, int64_t n, int64_
   HIPCHK(hipLaunchKernel(ka, dim3((unsigned)blocks_a), dim3(BLOCK), args_a, 0, stream));
   void* args_b[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&W, (void*)&ds, (void*)&lds,
                     (void*)&dm, (void*)&ldm, (void*)&dstat, (void*)&ns};
-  static const int occ = [] {
-    const char* e = getenv("RYD_JP_OCC");
-    return (e && e[0] == '3') ? 3 : 4;
-  }();
-  const void* kb = occ == 3 ? (const void*)jp_frame_kernel<3> : (const void*)jp_frame_kernel<4>;
+  // SYM holds 157 VGPRs (3 waves per SIMD; a 128 budget spills), the 4-output form 127
+  const void* kb = sym ? (const void*)jp_frame_kernel<3, true> : (const void*)jp_frame_kernel<4, false>;
   HIPCHK(hipLaunchKernel(kb, dim3((unsigned)blocks_b), dim3(BLOCK), args_b, 0, stream));
   HIPCHK(hipFreeAsync(W, stream));
   return RYD_OK;
