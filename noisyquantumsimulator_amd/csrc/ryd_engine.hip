@@ -2049,13 +2049,11 @@ int validate(const ryd_batch_desc* d, int64_t n, int64_t ldp, int64_t lds, int64
   return RYD_OK;
 }
 
-// RYD_JP_SPLIT=0 keeps smooth JP in the fused lindblad_prop_kernel (A/B measurements)
+// RYD_JP_SPLIT=0 keeps smooth JP in the fused lindblad_prop_kernel (A/B measurements and
+// the split-vs-fused bit-identity test); read at every launch
 bool jp_split_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RYD_JP_SPLIT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = getenv("RYD_JP_SPLIT");
+  return !(e && e[0] == '0');
 }
 
 // Smooth JP, propagator method: jp_rows_kernel -> workspace (25 x 25 doubles per

@@ -49,3 +49,24 @@ def test_c3_shard_properties():
     rho = r.rho()
     np.testing.assert_allclose(np.einsum("nkaa->nk", rho), 1.0, atol=1e-11)
     assert np.linalg.eigvalsh(rho[::50]).min() > -1e-11
+
+
+@pytest.mark.parametrize("symmetric", [True, False])
+def test_c3_split_kernels_bit_identical_to_fused(monkeypatch, symmetric):
+    """The two-launch smooth-JP path (jp_rows_kernel -> jp_frame_kernel, one output per
+    lane and the |10> mirror for identical atoms) performs the fused kernel's arithmetic
+    in the same order: states, summary and status must agree bit for bit."""
+    warnings.simplefilter("ignore")
+    b = SW.pareto_tgate_grid(n_omega=20, n_tau=13)          # 260 points: ragged last blocks
+    p = SW.c3_four_op_params(b).copy()
+    if not symmetric:                                      # unequal atoms: 4 outputs per lane
+        p[E.N.P["G1_B"]] *= 1.37
+    assert E.symmetric_atoms(p) == symmetric
+    eng = E.Engine()
+    monkeypatch.setenv("RYD_JP_SPLIT", "1")
+    rs = eng.run(p, "smooth_jp", "lindblad", n_steps=300)
+    monkeypatch.setenv("RYD_JP_SPLIT", "0")
+    rf = eng.run(p, "smooth_jp", "lindblad", n_steps=300)
+    assert np.all(rs.status == 0) and np.array_equal(rs.status, rf.status)
+    np.testing.assert_array_equal(rs.state, rf.state)
+    np.testing.assert_array_equal(rs.summary, rf.summary)
