@@ -1345,8 +1345,8 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
 // Split: jp_rows_kernel builds the phase-0 propagator (build_propagator, as above)
 // and writes each lane's row to a workspace; jp_frame_kernel walks the segments with
 // two points per wave (32 lanes each, 25 used), so every exchange is wave-local (no
-// s_barrier), ~100 VGPRs and 21 KB LDS per block (several blocks per CU hide the
-// LDS latency).  Same operands and operation order as the fused path: same bits.
+// s_barrier), 21 KB LDS per block.  Unequal atoms: the fused path's operands and
+// operation order, same bits.
 constexpr int FPW = 2;                       // points per wave (frame kernel)
 constexpr int FPB = FPW * (BLOCK / 64);      // 8 points per block
 constexpr int FCH = 64;                      // segments per wave-local phase-table chunk
@@ -1401,9 +1401,11 @@ __global__ __launch_bounds__(BLOCK, 2) void jp_rows_kernel(
 // Identical atoms (SYM): each 32-lane half is one point with one output per lane --
 // lanes 0..24 |11><11| row j (reads R_11), 25..29 |01><01| row j-25 (reads R_01, row
 // zeroed outside (0, m)), 30 |00><00| (row 0, column 0) -- 25 products a lane instead
-// of 36.  |10><10| is the atom-swap mirror of |01><01|, bit for bit (U[5a][5b] and
-// U[a][b] come from the same symmetric-block expression, the row rotation acts on the
-// same index pair), so lane 25 + r writes it too.
+// of 36.  |10><10| is the atom-swap mirror of |01><01| (U[5a][5b] and U[a][b] come
+// from the same symmetric-block expression, the row rotation acts on the same index
+// pair), so lane 25 + r writes it too.  Coordinates outside an input's invariant
+// support stay exactly zero here; the fused kernel leaves the ~1e-17-relative residue
+// of the sym/antisym recombination there (tests/test_gpu_c3.py).
 template <int OCC, bool SYM>                 // OCC: waves per SIMD the register budget targets
 __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, const double* __restrict__ W,
