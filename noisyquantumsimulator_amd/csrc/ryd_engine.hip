@@ -1031,22 +1031,22 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
     const int ra = j / 5, rb = j % 5;
     const int lo = ra < rb ? ra : rb, hi = ra < rb ? rb : ra;
     const int sr = sym_index(lo, hi);
-    const double wsr = (ra == rb) ? 1.0 : RSQRT2;
-    const int ar_ = (ra == rb) ? 0 : asym_index(lo, hi);
-    const double war = (ra == rb) ? 0.0 : (ra < rb ? RSQRT2 : -RSQRT2);
     const double* Us = Ub;
-    (void)ar_;
 #pragma unroll
     for (int m = 0; m < NC; ++m) {
       const int ca = m / 5, cb = m % 5;
       const int clo = ca < cb ? ca : cb, chi = ca < cb ? cb : ca;
-      const double wsc = (ca == cb) ? 1.0 : RSQRT2;
-      const double wac = (ca == cb) ? 0.0 : (ca < cb ? RSQRT2 : -RSQRT2);
-      double val = wsr * wsc * Us[sr * NS + sym_index(clo, chi)];
+      // basis-change weights with (1/sqrt2)^2 taken as exactly 1/2 (RSQRT2 * RSQRT2 is
+      // 0.5000000000000001): the symmetric and antisymmetric parts of an entry between
+      // the two different invariant subspaces (atom A vs atom B in |0><0|) then cancel
+      // to an exact zero instead of a rounding residue
+      const double wsym = (ra == rb) ? ((ca == cb) ? 1.0 : RSQRT2) : ((ca == cb) ? RSQRT2 : 0.5);
+      const double wanti = (ra == rb || ca == cb) ? 0.0 : (((ra < rb) == (ca < cb)) ? 0.5 : -0.5);
+      double val = wsym * Us[sr * NS + sym_index(clo, chi)];
       // antisymmetric part: on the (0, m) coordinates it is the single-atom block B
       // (Ua[(0,hi)][(0,chi)] = Us[(0,hi)][(0,chi)] = Us[hi][chi]); elsewhere the basis
       // inputs never have support, so it is left out
-      if (ca != cb && lo == 0 && clo == 0) val = fma(war * wac, Us[hi * NS + chi], val);
+      if (ca != cb && lo == 0 && clo == 0) val = fma(wanti, Us[hi * NS + chi], val);
       u[m] = val;
     }
   }
@@ -1345,8 +1345,8 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
 // Split: jp_rows_kernel builds the phase-0 propagator (build_propagator, as above)
 // and writes each lane's row to a workspace; jp_frame_kernel walks the segments with
 // two points per wave (32 lanes each, 25 used), so every exchange is wave-local (no
-// s_barrier), 21 KB LDS per block.  Unequal atoms: the fused path's operands and
-// operation order, same bits.
+// s_barrier), 21 KB LDS per block.  Same operands and operation order as the fused
+// path (identical atoms: its terms that are exact zeros skipped), same bits.
 constexpr int FPW = 2;                       // points per wave (frame kernel)
 constexpr int FPB = FPW * (BLOCK / 64);      // 8 points per block
 constexpr int FCH = 64;                      // segments per wave-local phase-table chunk
@@ -1403,9 +1403,9 @@ __global__ __launch_bounds__(BLOCK, 2) void jp_rows_kernel(
 // zeroed outside (0, m)), 30 |00><00| (row 0, column 0) -- 25 products a lane instead
 // of 36.  |10><10| is the atom-swap mirror of |01><01| (U[5a][5b] and U[a][b] come
 // from the same symmetric-block expression, the row rotation acts on the same index
-// pair), so lane 25 + r writes it too.  Coordinates outside an input's invariant
-// support stay exactly zero here; the fused kernel leaves the ~1e-17-relative residue
-// of the sym/antisym recombination there (tests/test_gpu_c3.py).
+// pair), so lane 25 + r writes it too.  Entries of U between the two invariant
+// subspaces are exact zeros (build_propagator step 3), so this equals the fused
+// kernel's full sums bit for bit (tests/test_gpu_c3.py).
 template <int OCC, bool SYM>                 // OCC: waves per SIMD the register budget targets
 __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, const double* __restrict__ W,
