@@ -34,6 +34,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (spec)
 # FLOPs per generator application (one 25-vector): apply_A 75 + apply_B 75 + V 12 + Clenshaw 25 FMAs
 FLOP_PER_MATVEC = 2 * (75 + 75 + 12 + 25)
+# identical atoms: the symmetric column on its 15-entry triangle (apply_Lsym): every
+# output (i <= j) costs row i + row j of M (1, 3, 3, 4, 4 ops), V 6, Clenshaw 15
+FLOP_PER_MATVEC_SYM = 2 * (6 * (1 + 3 + 3 + 4 + 4) + 6 + 15)
 FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
 # identical atoms: only the block-triangular symmetric block [[B, C], [0, D]] (5 + 10):
 # B^2 (125) + BC + CD (250 + 500) + D^2 (1000) FMAs
@@ -243,7 +246,8 @@ def main():
     nsq = float(res.col("NSQUARE").sum())
     prop_kernel = args.method in ("cheb_squaring", "chebyshev")   # both workloads: auto -> prop
     sq_flops = FLOP_PER_SQUARING_SYM if E.symmetric_atoms(params) else FLOP_PER_SQUARING
-    flops = res.matvec_useful * FLOP_PER_MATVEC + nsq * sq_flops
+    mv_flops = FLOP_PER_MATVEC_SYM if E.symmetric_atoms(params) else FLOP_PER_MATVEC
+    flops = res.matvec_useful * mv_flops + nsq * sq_flops
     if prop_kernel:
         upd = FLOP_PER_STATE_UPDATE_SYM if E.symmetric_atoms(params) else FLOP_PER_STATE_UPDATE
         flops += n_seg * n * upd                         # R <- U R once per reference segment

@@ -273,6 +273,48 @@ __device__ __forceinline__ void apply_V(double vs, const double (&b)[25], double
   o[3 * 5 + 4] = fma(-vs, b[4 * 5 + 4], o[3 * 5 + 4]);
 }
 
+__host__ __device__ constexpr int sym_index(int i, int j) {      // i <= j
+  return i * 5 - i * (i - 1) / 2 + (j - i);
+}
+
+// Identical atoms, exchange-symmetric R (R[i][j] = R[j][i]) stored as its upper
+// triangle t[sym_index(i, j)], i <= j.  o(i,j) += (M R)(i,j) + (R M^T)(i,j) + V(R)(i,j):
+// the A part (row i of M on column j of R) then the B part (row j of M on row i), as
+// apply_A/apply_B accumulate them, on 15 outputs instead of 25 (95 FMAs, not 162).
+__host__ __device__ constexpr int tri(int i, int j) { return i <= j ? sym_index(i, j) : sym_index(j, i); }
+
+// o += sum_c M[r][c] u[c] with apply_A's fma order for row r (u = a column of R)
+__device__ __forceinline__ double mrow(const Gen& a, int r, double u1, double u2, double u3, double u4,
+                                       double o) {
+  switch (r) {
+    case 0: return fma(a.g0, u2, o);
+    case 1: return fma(a.g1, u2, fma(a.hy2, u3, fma(-a.hx2, u4, o)));
+    case 2: return fma(a.mg01, u2, fma(-a.hy2, u3, fma(a.hx2, u4, o)));
+    case 3: return fma(a.hy, u2 - u1, fma(-a.G, u3, fma(a.hz2, u4, o)));
+    default: return fma(a.hx, u1 - u2, fma(-a.hz2, u3, fma(-a.G, u4, o)));
+  }
+}
+
+__device__ __forceinline__ void apply_Lsym(const Gen& a, double vs, const double (&t)[15], double (&o)[15]) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = i; j < 5; ++j) {
+      const int s = sym_index(i, j);
+      double acc = mrow(a, i, t[tri(1, j)], t[tri(2, j)], t[tri(3, j)], t[tri(4, j)], o[s]);
+      o[s] = mrow(a, j, t[tri(i, 1)], t[tri(i, 2)], t[tri(i, 3)], t[tri(i, 4)], acc);
+    }
+  // V P_rr on the symmetric triangle (apply_V's S (x) D + D (x) S, both halves summed)
+  const double v2 = 2.0 * vs;
+  const double r23 = t[tri(2, 3)], r24 = t[tri(2, 4)], r33 = t[tri(3, 3)], r34 = t[tri(3, 4)],
+               r44 = t[tri(4, 4)];
+  o[tri(2, 3)] = fma(-v2, r24, o[tri(2, 3)]);
+  o[tri(2, 4)] = fma(v2, r23, o[tri(2, 4)]);
+  o[tri(3, 3)] = fma(-v2, r34, o[tri(3, 3)]);
+  o[tri(3, 4)] = fma(-vs, r44, fma(vs, r33, o[tri(3, 4)]));
+  o[tri(4, 4)] = fma(v2, r34, o[tri(4, 4)]);
+}
+
 template <bool SYM>
 __device__ __forceinline__ void apply_L(const Gen& a, const Gen& b2, double vs, const double (&b)[25],
                                         double (&o)[25]) {
@@ -857,9 +899,6 @@ __device__ __forceinline__ void segment_phase(const PointP& q, int s, int n_step
 // so in the orthonormal basis {sym_s = (E_ij + E_ji)/sqrt2 (i<j), E_ii ; asym_a =
 // (E_ij - E_ji)/sqrt2 (i<j)} the propagator is block-diagonal, U = Us (15x15) (+)
 // Ua (10x10).  A squaring then costs 15^3 + 10^3 = 4375 FMAs instead of 25^3.
-__host__ __device__ constexpr int sym_index(int i, int j) {      // i <= j
-  return i * 5 - i * (i - 1) / 2 + (j - i);
-}
 __host__ __device__ constexpr int asym_index(int i, int j) {     // i < j
   return i * 4 - i * (i - 1) / 2 + (j - i - 1);
 }
@@ -909,28 +948,37 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
   const double w0 = SYM ? ((bi == bj) ? 1.0 : RSQRT2) : 1.0;
   const int e1 = SYM ? 5 * bi + bj : j, e2 = SYM ? 5 * bj + bi : j;
   const double w2 = SYM ? (is_sym ? w0 : -w0) : 0.0;
-  // (1) column of exp(y Y)
-  double v[25];
+  // (1) column of exp(y Y).  SYM: only the 15 symmetric columns are needed (see the
+  // squaring below), and a symmetric column stays symmetric: it runs on the 15-entry
+  // upper triangle (apply_Lsym)
+  constexpr int NV = SYM ? NS : 25;
+  double v[NV];
 #pragma unroll
-  for (int e = 0; e < 25; ++e) v[e] = (e == e1) ? w0 : ((e == e2) ? w2 : 0.0);
-  // SYM: only the 15 symmetric columns are needed (see the squaring below)
-  cheb_segment<25>(v, y, active && (!SYM || is_sym),
-                   [&](const double (&b)[25], double (&o)[25]) { apply_L<SYM>(A, B, vs, b, o); },
-                   nuse, nexec);
+  for (int e = 0; e < NV; ++e) v[e] = SYM ? ((e == j) ? w0 : 0.0) : ((e == e1) ? w0 : ((e == e2) ? w2 : 0.0));
+  if constexpr (SYM) {
+    (void)B;
+    cheb_segment<NS>(v, y, active && is_sym,
+                     [&](const double (&b)[NS], double (&o)[NS]) { apply_Lsym(A, vs, b, o); }, nuse, nexec);
+  } else {
+    cheb_segment<25>(v, y, active,
+                     [&](const double (&b)[25], double (&o)[25]) { apply_L<SYM>(A, B, vs, b, o); }, nuse,
+                     nexec);
+  }
   if (t == 0) s_max = 0;
   __syncthreads();
   double* Ub = &U[pl][0][0];
   if (lane_ok) {
-    if (!SYM) {
+    if constexpr (!SYM) {
 #pragma unroll
       for (int r = 0; r < 25; ++r) U[pl][r][j] = v[r];
-    } else if (is_sym) {                    // Us[s'][j] = <sym_s', v>
+    } else if (is_sym) {                    // Us[s'][j] = <sym_s', v> = sqrt2 R[i2][j2] off the diagonal
 #pragma unroll
       for (int i2 = 0; i2 < 5; ++i2)
 #pragma unroll
-        for (int j2 = i2; j2 < 5; ++j2)
-          Ub[sym_index(i2, j2) * NS + j] =
-              (i2 == j2) ? v[5 * i2 + i2] : RSQRT2 * (v[5 * i2 + j2] + v[5 * j2 + i2]);
+        for (int j2 = i2; j2 < 5; ++j2) {
+          const double r = v[sym_index(i2, j2)];
+          Ub[sym_index(i2, j2) * NS + j] = (i2 == j2) ? r : RSQRT2 * (r + r);
+        }
     }
     // (SYM: the antisymmetric block is not built -- see the squaring below)
     atomicMax(&s_max, sq);
