@@ -865,6 +865,9 @@ __global__ __launch_bounds__(BLOCK) void lindblad4_cheb_kernel(
 // Q(phi_s - phi_{s+1}).  LP uses the frame only when |xi| = 1 to 1e-14 for the
 // whole block (xi from compute_phase_shift_xi always is; an ABI caller may pass
 // any xi), otherwise it builds both propagators.
+#ifndef RYD_PROP_OCC_SYM
+#define RYD_PROP_OCC_SYM 3                  // waves per SIMD targeted by the identical-atom propagator kernel (168 VGPRs, a few setup spills)
+#endif
 constexpr int PPB = 10;                     // points per 256-lane block (250 lanes used)
 constexpr int NC = 25;
 // Chebyshev argument after scaling.  Lower means fewer Chebyshev terms and more
@@ -910,8 +913,12 @@ constexpr int NS = 15;                       // symmetric coordinates (the 10 an
 // squaring) and return this lane's row j of U (full 25-coordinate form) in u.
 // Without SYM, U[p] holds the 25x25 matrix; with SYM its first 325 doubles hold
 // Us (15x15, row-major) then Ua (10x10).
+// LDS doubles per point for the propagator: the 15x15 symmetric block, or the 25x25 U
 template <bool SYM>
-__device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& s_max, const PointP& q,
+constexpr int u_size() { return SYM ? NS * NS : NC * NC; }
+
+template <bool SYM>
+__device__ __forceinline__ void build_propagator(double (&U)[PPB][u_size<SYM>()], int& s_max, const PointP& q,
                                                  const Seg& g, bool valid, bool lane_ok, int t, int pl,
                                                  int j, double& nuse, double& nexec, double& nsq,
                                                  bool& over_cap, double (&u)[NC]) {
@@ -966,11 +973,11 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
   }
   if (t == 0) s_max = 0;
   __syncthreads();
-  double* Ub = &U[pl][0][0];
+  double* Ub = &U[pl][0];
   if (lane_ok) {
     if constexpr (!SYM) {
 #pragma unroll
-      for (int r = 0; r < 25; ++r) U[pl][r][j] = v[r];
+      for (int r = 0; r < 25; ++r) Ub[r * NC + j] = v[r];
     } else if (is_sym) {                    // Us[s'][j] = <sym_s', v> = sqrt2 R[i2][j2] off the diagonal
 #pragma unroll
       for (int i2 = 0; i2 < 5; ++i2)
@@ -1074,7 +1081,7 @@ __device__ __forceinline__ void build_propagator(double (&U)[PPB][NC][NC], int& 
   // (3) this lane's row of U in full coordinates
   if (!SYM) {
 #pragma unroll
-    for (int m = 0; m < NC; ++m) u[m] = U[pl][j][m];
+    for (int m = 0; m < NC; ++m) u[m] = Ub[j * NC + m];
   } else {
     const int ra = j / 5, rb = j % 5;
     const int lo = ra < rb ? ra : rb, hi = ra < rb ? rb : ra;
@@ -1208,10 +1215,10 @@ __device__ __forceinline__ void rotate_coord(const double (&src)[4][NC], double 
 }
 
 template <int PROTO, bool SYM>
-__global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
+__global__ __launch_bounds__(BLOCK, SYM ? RYD_PROP_OCC_SYM : 2) void lindblad_prop_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ st, int64_t lds,
     double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
-  __shared__ __attribute__((aligned(16))) double U[PPB][NC][NC];    // row-major U[p][row][col]
+  __shared__ __attribute__((aligned(16))) double U[PPB][u_size<SYM>()];   // per point: Us (SYM) or row-major U
   __shared__ __attribute__((aligned(16))) double Rs[PPB][4][NC];    // basis-input states
   __shared__ __attribute__((aligned(16))) double Rt[PPB][4][NC];    // rotated states (frame path)
   __shared__ int s_max;
@@ -1278,9 +1285,9 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
     // reuses U's LDS (free now: each lane holds its row) instead of redundantly by
     // the point's 25 lanes every segment; same arithmetic, so the same bits.
     constexpr bool TAB = PROTO == RYD_PROTO_SMOOTH_JP;
-    constexpr int CH = (NC * NC) / 2;        // segments per table chunk (312)
-    static_assert(2 * CH <= NC * NC, "phase table must fit in U");
-    double* ph = &U[0][0][0];                // ph[(p * CH + s % CH) * 2 + {0: cos, 1: sin}]
+    constexpr int CH = u_size<SYM>() / 2;    // segments per table chunk (112 SYM, 312)
+    static_assert(2 * CH <= u_size<SYM>(), "phase table must fit in U");
+    double* ph = &U[0][0];                   // ph[(p * CH + s % CH) * 2 + {0: cos, 1: sin}]
     for (int s = 0; s < nseg; ++s) {
       double c, sn;
       if (TAB) {
@@ -1310,14 +1317,13 @@ __global__ __launch_bounds__(BLOCK, 2) void lindblad_prop_kernel(
       // the lane's row; the states ping-pong between Rs and Rt (one barrier a segment)
       const double cr = cp * c + sp * sn, sr = sp * c - cp * sn;
       if (lane_ok) {
-        double ur[NC], nr[4];
-        rot_row(u, cr, sr, ur);
+        double nr[4];
         if ((s & 1) == 0) {
-          update_rows(ur, Rs[pl], nr);
+          update_rows_rot(u, cr, sr, Rs[pl], nr);
 #pragma unroll
           for (int k = 0; k < 4; ++k) Rt[pl][k][j] = nr[k];
         } else {
-          update_rows(ur, Rt[pl], nr);
+          update_rows_rot(u, cr, sr, Rt[pl], nr);
 #pragma unroll
           for (int k = 0; k < 4; ++k) Rs[pl][k][j] = nr[k];
         }
@@ -1413,7 +1419,7 @@ __global__ __launch_bounds__(BLOCK, 2) void jp_rows_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ W,
     double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
   constexpr int PROTO = RYD_PROTO_SMOOTH_JP;
-  __shared__ __attribute__((aligned(16))) double U[PPB][NC][NC];
+  __shared__ __attribute__((aligned(16))) double U[PPB][u_size<SYM>()];
   __shared__ int s_max;
   const int t = threadIdx.x;
   const bool lane_ok = t < PPB * NC;
