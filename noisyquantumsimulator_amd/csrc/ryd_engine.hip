@@ -1123,32 +1123,12 @@ __device__ __forceinline__ void update_rows(const double (&u)[NC], const double 
   for (int m = 0; m < NC; ++m) nr[3] = fma(u[m], R[3][m], nr[3]);
 }
 
-// o = (Q1 (x) Q1)^T u for a propagator row u, so that o . R = u . (Q R): the frame
-// rotation of rotate_coord moved onto the lane's own row (registers only).  Q1 mixes
-// the (ex, ey) coordinates 3, 4: rows [c s; -s c].
-__device__ __forceinline__ void rot_row(const double (&u)[NC], double c, double s, double (&o)[NC]) {
-  double t[NC];
-#pragma unroll
-  for (int b = 0; b < 5; ++b) {
-    t[b] = u[b];
-    t[5 + b] = u[5 + b];
-    t[10 + b] = u[10 + b];
-    t[15 + b] = fma(c, u[15 + b], -s * u[20 + b]);
-    t[20 + b] = fma(s, u[15 + b], c * u[20 + b]);
-  }
-#pragma unroll
-  for (int a = 0; a < 5; ++a) {
-    o[5 * a] = t[5 * a];
-    o[5 * a + 1] = t[5 * a + 1];
-    o[5 * a + 2] = t[5 * a + 2];
-    o[5 * a + 3] = fma(c, t[5 * a + 3], -s * t[5 * a + 4]);
-    o[5 * a + 4] = fma(s, t[5 * a + 3], c * t[5 * a + 4]);
-  }
-}
-
-// update_rows(rot_row(u, c, s), R): the rotated row produced one atom-A index a at a
-// time and consumed at once (ascending coordinate order, the same expressions), so
-// the 25 rotated coefficients are never live together -- same bits, fewer VGPRs.
+// update_rows with the row rotated first: o = (Q1 (x) Q1)^T u for a propagator row u,
+// so that o . R = u . (Q R) -- the frame rotation of rotate_coord moved onto the lane's
+// own row (registers only).  Q1 mixes the (ex, ey) coordinates 3, 4: rows [c s; -s c]
+// (t: the atom-A index pass, then the atom-B pass).  The rotated row is produced one
+// atom-A index a at a time and consumed at once (ascending coordinate order), so the 25
+// rotated coefficients are never live together.
 __device__ __forceinline__ void update_rows_rot(const double (&u)[NC], double c, double s,
                                                 const double (&R)[4][NC], double (&nr)[4]) {
   nr[0] = nr[1] = nr[2] = nr[3] = 0.0;
@@ -1175,7 +1155,7 @@ __device__ __forceinline__ void update_rows_rot(const double (&u)[NC], double c,
   }
 }
 
-// One basis input only: sum_m o[m] R[m] with o = rot_row(u, c, s) (the nr[3] chain of
+// One basis input only: sum_m o[m] R[m] with o the rotated row (the nr[3] chain of
 // update_rows_rot; with u zero outside an input's support the extra terms are exact zeros).
 __device__ __forceinline__ double update_row_rot(const double (&u)[NC], double c, double s,
                                                  const double* __restrict__ R) {
