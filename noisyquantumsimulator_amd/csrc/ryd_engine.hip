@@ -866,7 +866,7 @@ __global__ __launch_bounds__(BLOCK) void lindblad4_cheb_kernel(
 // whole block (xi from compute_phase_shift_xi always is; an ABI caller may pass
 // any xi), otherwise it builds both propagators.
 #ifndef RYD_PROP_OCC_SYM
-#define RYD_PROP_OCC_SYM 3                  // waves per SIMD targeted by the identical-atom propagator kernel (168 VGPRs, a few setup spills)
+#define RYD_PROP_OCC_SYM 3                  // waves per SIMD for the identical-atom LP-square propagator kernel (168 VGPRs, a few spills; measured C2/C4); other protocols keep 2
 #endif
 constexpr int PPB = 10;                     // points per 256-lane block (250 lanes used)
 constexpr int NC = 25;
@@ -1195,7 +1195,7 @@ __device__ __forceinline__ void rotate_coord(const double (&src)[4][NC], double 
 }
 
 template <int PROTO, bool SYM>
-__global__ __launch_bounds__(BLOCK, SYM ? RYD_PROP_OCC_SYM : 2) void lindblad_prop_kernel(
+__global__ __launch_bounds__(BLOCK, (SYM && PROTO == RYD_PROTO_LP_SQUARE) ? RYD_PROP_OCC_SYM : 2) void lindblad_prop_kernel(
     const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ st, int64_t lds,
     double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
   __shared__ __attribute__((aligned(16))) double U[PPB][u_size<SYM>()];   // per point: Us (SYM) or row-major U
