@@ -45,6 +45,9 @@ FLOP_PER_SQUARING_SYM = 2 * (5 ** 3 + 5 * 5 * 10 + 5 * 10 * 10 + 10 ** 3)
 # |01>/|10>: 5x5, |11>: 25x25); identical atoms: |10> is the atom-swap mirror of |01>
 FLOP_PER_STATE_UPDATE = 2 * (1 + 25 + 25 + 625)
 FLOP_PER_STATE_UPDATE_SYM = 2 * (1 + 25 + 625)
+# the 16-lane DPP-row kernel (csrc/ryd_sym16.inc) keeps |11> on its 15-coordinate exchange-
+# symmetric triangle: 15 x 15 + the single-atom 5 x 5 (|01>, |10> its mirror) + |00>
+FLOP_PER_STATE_UPDATE_SYM16 = 2 * (1 + 25 + 225)
 N_OMEGA, N_DELTA = 100, 100
 # PMC-measured HBM bytes per launch of the dominant kernel (rocprofv3 --pmc FETCH_SIZE /
 # WRITE_SIZE in separate passes, FETCH_SIZE x2 per MI355X_MICROARCH.md), committed under
@@ -248,8 +251,13 @@ def main():
     sq_flops = FLOP_PER_SQUARING_SYM if E.symmetric_atoms(params) else FLOP_PER_SQUARING
     mv_flops = FLOP_PER_MATVEC_SYM if E.symmetric_atoms(params) else FLOP_PER_MATVEC
     flops = res.matvec_useful * mv_flops + nsq * sq_flops
+    sym16 = (args.method == "chebyshev" and E.symmetric_atoms(params)
+             and os.environ.get("RYD_SYM16", "1") != "0")
     if prop_kernel:
-        upd = FLOP_PER_STATE_UPDATE_SYM if E.symmetric_atoms(params) else FLOP_PER_STATE_UPDATE
+        if sym16:
+            upd = FLOP_PER_STATE_UPDATE_SYM16
+        else:
+            upd = FLOP_PER_STATE_UPDATE_SYM if E.symmetric_atoms(params) else FLOP_PER_STATE_UPDATE
         flops += n_seg * n * upd                         # R <- U R once per reference segment
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     tr = _measured_traffic(args.workload, args.method, n)
@@ -276,7 +284,8 @@ def main():
         "data": "synthetic",
         "config": {"workload": workload, "points_per_gpu": n, "global_points": global_points,
                    "parallelism": f"range-shard x{ws}",
-                   "method": args.method + (" (auto: propagator kernel, phase frame)"
+                   "method": args.method + ((" (auto: 16-lane DPP-row propagator kernel, phase frame)"
+                                             if sym16 else " (auto: propagator kernel, phase frame)")
                                             if args.method == "chebyshev" else "")},
         # The binding roof is FP64 arithmetic (MI355X dense FP64: 78.6 TF, the same for the
         # matrix cores and the VALU; these kernels run on the FP64 VALU); the HBM view is

@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/ryd_engine.h"
@@ -189,10 +190,18 @@ __device__ __forceinline__ int cheb_terms(double x) {
   return (int)ceil(x + 12.0 * cbrt(x) + 10.0);
 }
 
+// Max over the wave: DPP within each 16-lane row (quad swaps, half-row and row
+// mirrors), then the four row results through readlane -- ALU only (the
+// __shfl_xor form goes through ds_bpermute, an LDS round trip per step).  Call with
+// every lane active.
 __device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-  return v;
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));  // row_mirror
+  const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return max(max(a, b), max(c, d));
 }
 
 // ---------------------------------------------------------------------------
@@ -1561,6 +1570,11 @@ __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
   }
 }
 
+#ifndef RYD_S16_WAVES
+#define RYD_S16_WAVES 3                      // waves per SIMD the sym16 register budget targets
+#endif
+#include "ryd_sym16.inc"
+
 // ---------------------------------------------------------------------------
 // Adaptive Dormand-Prince 5(4) kernel (RYD_METHOD_DOPRI5)
 // ---------------------------------------------------------------------------
@@ -2000,6 +2014,19 @@ bool use_propagator(const ryd_batch_desc* d) {
          (d->method == RYD_METHOD_CHEB_SQUARING || (d->method == RYD_METHOD_CHEBYSHEV && auto_prop));
 }
 
+// Identical atoms under the auto method (LP square, bang-bang, smooth JP): the
+// 16-lane DPP-row kernel of ryd_sym16.inc.  RYD_SYM16=0 falls back to
+// lindblad_prop_kernel / the smooth-JP split pair (A/B measurements, tests); the
+// explicit RYD_METHOD_CHEB_SQUARING always runs those.
+bool use_sym16(const ryd_batch_desc* d) {
+  const char* e = getenv("RYD_SYM16");
+  if (e && e[0] == '0') return false;
+  return d->dim == 3 && d->evolution == RYD_EVOL_LINDBLAD && d->method == RYD_METHOD_CHEBYSHEV &&
+         (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0 &&
+         (d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG ||
+          d->protocol == RYD_PROTO_SMOOTH_JP);
+}
+
 KernelFn pick_kernel(const ryd_batch_desc* d) {
   const bool sym = (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0;
   if (d->dim == 4) {
@@ -2144,6 +2171,20 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
                     (void*)&ldm, (void*)&dstat, (void*)&ns, (void*)&sh, (void*)&rt, (void*)&at,
                     (void*)&ms};
     HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(DP_BLOCK), args, 0, stream));
+    return RYD_OK;
+  }
+  if (use_sym16(d)) {
+    using SFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, double*, int64_t, uint32_t*,
+                         int, int);
+    SFn f = d->protocol == RYD_PROTO_LP_SQUARE ? lindblad_sym16_kernel<RYD_PROTO_LP_SQUARE>
+            : d->protocol == RYD_PROTO_SMOOTH_JP ? lindblad_sym16_kernel<RYD_PROTO_SMOOTH_JP>
+                                                  : lindblad_sym16_kernel<RYD_PROTO_BANGBANG>;
+    const int64_t blocks = (n + S16_PPW - 1) / S16_PPW;
+    if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
+    int ns = d->n_steps, sh = d->shape;
+    void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
+                    (void*)&ldm, (void*)&dstat, (void*)&ns, (void*)&sh};
+    HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(S16_BLOCK), args, 0, stream));
     return RYD_OK;
   }
   if (use_propagator(d) && d->protocol == RYD_PROTO_SMOOTH_JP && jp_split_enabled())
