@@ -62,6 +62,21 @@ def _penalty(cp):
     return err, np.cos(err / 2) ** 2
 
 
+def compute_state_fidelity(psi_out: np.ndarray, psi_target: np.ndarray) -> float:
+    """RG/simulation.py:186-222: |<t|psi>|^2 for two kets; otherwise the Uhlmann
+    fidelity qutip.fidelity(rho, sigma) = Tr sqrt(sqrt(rho) sigma sqrt(rho)), squared."""
+    a, b = np.asarray(psi_out), np.asarray(psi_target)
+    if a.ndim == 1 and b.ndim == 1:
+        return float(abs(np.vdot(b, a)) ** 2)
+    rho = np.outer(a, a.conj()) if a.ndim == 1 else a
+    sig = np.outer(b, b.conj()) if b.ndim == 1 else b
+    w, V = np.linalg.eigh((rho + rho.conj().T) / 2)
+    sq = (V * np.sqrt(np.clip(w, 0, None))) @ V.conj().T
+    m = sq @ sig @ sq
+    ev = np.linalg.eigvalsh((m + m.conj().T) / 2)
+    return float(np.sum(np.sqrt(np.clip(ev, 0, None))) ** 2)
+
+
 def compute_CZ_fidelity(results: Dict[str, np.ndarray], extract_global_phase: bool = True,
                         hilbert_space_dim: int = 3, eigh=None) -> Tuple[Dict[str, float], float, Dict]:
     """Per-state fidelities, average and phase_info, as RG/simulation.py:225-633."""
