@@ -199,10 +199,23 @@ typedef struct ryd_traj_desc {
   double psi0[2 * RYD_T_DIM];  /* normalised initial ket, (re, im) interleaved */
 } ryd_traj_desc;
 
-/* ---- per-point status bits ---- */
+/* ---- per-point status bits ----
+ * Set by the kernels (failures: the analogue of the reference's exceptions -> 1e6 /
+ * NaN sentinels): */
 #define RYD_STATUS_NONFINITE   1u
 #define RYD_STATUS_STEP_CAP    2u   /* DOPRI5 step cap (ZVODE nsteps analogue)          */
 #define RYD_STATUS_BAD_INPUT   4u   /* Omega <= 0, tau <= 0, nseg out of range ...      */
+#define RYD_STATUS_FAIL_MASK   7u
+/* Warnings (the reference's UserWarnings, per point instead of per call; set by the
+ * host layer's derivation, never by the kernels): */
+#define RYD_STATUS_WEAK_BLOCKADE  8u   /* LP: V/Omega < 10 (RG/protocols.py:615-619); smooth JP:
+                                          V/Omega < 5 (RG/simulation.py:1670-1676)          */
+#define RYD_STATUS_DARK_STATE_SIGN 16u /* smooth JP: delta/Omega of the wrong sign for the
+                                          intermediate detuning (RG/simulation.py:1631-1647) */
+#define RYD_STATUS_OMEGA_RANGE   32u   /* Omega/2pi > 100 MHz or < 0.1 MHz (:2930-2946)     */
+/* Set by ryd_mixed_phase: the reference's mixed-state phase penalty is not a function
+ * of rho at the checked precision (LAPACK eigenvector gauge, see below). */
+#define RYD_STATUS_GAUGE_UNSTABLE 64u
 
 typedef struct ryd_batch_desc {
     int32_t abi_version;     /* = RYD_ABI_VERSION */
@@ -290,6 +303,28 @@ int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* de
                                 double* d_rho, int64_t ld_rho, double* d_se, int64_t ld_se,
                                 double* d_summary, int64_t ld_summary, double* d_records,
                                 uint32_t* d_status, void* stream, float* elapsed_ms);
+
+/* ---- host epilogue: the reference's mixed-state controlled phase ----
+ * RG/simulation.py:424-452 takes, for each output rho_x (x = 00, 01, 10, 11), the
+ * eigenvector of the largest eigenvalue (rho.eigenstates(): QuTiP 5 -> scipy.linalg.
+ * eigh -> LAPACK zheevr, JOBZ 'V', RANGE 'A', UPLO 'L', ABSTOL 0) and its phase at
+ * |x>; cp = wrap(phi11 - phi01 - phi10 + phi00), penalty cos^2(err/2), err = min|cp -+
+ * pi| (:444-452).  Output: the component <x|v_max> per input (the phase is its angle).  `zheevr` is the caller's LAPACK zheevr (Fortran ABI, 32-bit ints;
+ * the Python layer passes scipy's, so the phases equal scipy.linalg.eigh's bit for
+ * bit).  `state` = Lindblad sector rows as ryd_run_batch writes them ([25 | 36][ld]).
+ * Gauge check: the same procedure on n_perturb copies with every sector coordinate
+ * scaled by (1 +- rel_eps); out_flags[i] |= RYD_STATUS_GAUGE_UNSTABLE if any penalty
+ * moves by more than tol.  Host only, n_threads worker threads (0 = all cores). */
+#define RYD_MP_V0       0   /* <x|v_max> as (re, im) row pairs, x = 00, 01, 10, 11; the
+                               phase is its angle (taken by the caller: the reference
+                               uses np.angle)                                       */
+#define RYD_MP_CTRL     8   /* wrapped controlled phase (libm atan2; gauge check)    */
+#define RYD_MP_PENALTY  9   /* cos^2(err / 2)                                       */
+#define RYD_MP_SPREAD   10  /* max |penalty(perturbed) - penalty|                   */
+#define RYD_MP_WIDTH    11
+int ryd_mixed_phase(void* zheevr, int dim, const double* state, int64_t n, int64_t ld_state,
+                    int n_perturb, double rel_eps, double tol, int n_threads,
+                    double* out, int64_t ld_out, uint32_t* out_flags);
 
 /* Minimal device-memory plumbing so callers need no other GPU runtime. */
 int ryd_malloc(ryd_handle* h, int slot, size_t bytes, void** d_ptr);

@@ -30,6 +30,12 @@ S = dict(POP0=0, OV_RE0=4, OV_IM0=8, AVG_POP=12, CTRL_PHASE=13, PENALTY=14, AVG_
          NMV_USEFUL=16, NMV_EXEC=17, TRACE11=18, NSQUARE=19)
 NSUMMARY = 20
 STATUS_NONFINITE, STATUS_STEP_CAP, STATUS_BAD_INPUT = 1, 2, 4
+STATUS_FAIL_MASK = 7                      # kernel failures; the bits below are warnings
+STATUS_WEAK_BLOCKADE, STATUS_DARK_STATE_SIGN, STATUS_OMEGA_RANGE = 8, 16, 32
+STATUS_GAUGE_UNSTABLE = 64
+# ryd_mixed_phase output rows
+MP = dict(V0=0, CTRL=8, PENALTY=9, SPREAD=10)
+MP_WIDTH = 11
 STATE_WIDTH = {"lindblad": 25, "ket": 18}                 # dim 3
 STATE_WIDTH_DIM = {3: STATE_WIDTH, 4: {"lindblad": 36, "ket": 32}}
 # process-map coherence rows (ryd_run_coherences)
@@ -47,6 +53,7 @@ EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary
             "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",
             "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
             "ryd_run_trajectories", "ryd_run_trajectories_device",
+            "ryd_mixed_phase",
             "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize")
 
 
@@ -113,6 +120,8 @@ def load() -> ctypes.CDLL:
         lib.ryd_run_trajectories_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(TrajDesc), vp, i64, i64,
                                                     i64, vp, i64, vp, i64, vp, i64, vp, vp, vp,
                                                     ctypes.POINTER(ctypes.c_float)]
+        lib.ryd_mixed_phase.argtypes = [vp, ctypes.c_int, dp, i64, i64, ctypes.c_int, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_int, dp, i64, ctypes.POINTER(ctypes.c_uint32)]
         lib.ryd_malloc.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]
         lib.ryd_free.argtypes = [vp, ctypes.c_int, vp]
         lib.ryd_memcpy_h2d.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]
@@ -130,3 +139,22 @@ def check(rc: int) -> None:
     if rc != RYD_OK:
         msg = load().ryd_last_error().decode(errors="replace")
         raise EngineError(f"ryd_engine error {rc}: {msg}")
+
+
+_zheevr = None
+
+
+def scipy_zheevr() -> int:
+    """Address of scipy's own LAPACK zheevr (scipy.linalg.cython_lapack), the routine
+    scipy.linalg.eigh -- and through it QuTiP 5's Qobj.eigenstates -- calls."""
+    global _zheevr
+    if _zheevr is None:
+        from scipy.linalg import cython_lapack
+        cap = cython_lapack.__pyx_capi__["zheevr"]
+        api = ctypes.pythonapi
+        api.PyCapsule_GetName.restype = ctypes.c_char_p
+        api.PyCapsule_GetName.argtypes = [ctypes.py_object]
+        api.PyCapsule_GetPointer.restype = ctypes.c_void_p
+        api.PyCapsule_GetPointer.argtypes = [ctypes.py_object, ctypes.c_char_p]
+        _zheevr = api.PyCapsule_GetPointer(cap, api.PyCapsule_GetName(cap))
+    return _zheevr

@@ -30,7 +30,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -2365,6 +2367,9 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
 
 // three-atom quantum-jump trajectories (BASELINE configs[4])
 #include "ryd_traj.inc"
+
+// host epilogue: the reference's mixed-state controlled phase (ryd_mixed_phase)
+#include "ryd_epilogue.inc"
 
 }  // namespace
 

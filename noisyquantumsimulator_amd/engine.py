@@ -13,6 +13,7 @@ want ``SimulationResult.results``.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Optional, Sequence, Tuple
 
@@ -51,6 +52,35 @@ def expand_ket(state: np.ndarray, n: int, dim: int = 3) -> np.ndarray:
     D = dim * dim
     s = state[:2 * D, :4 * n]
     return (s[0::2] + 1j * s[1::2]).T.reshape(n, 4, D)
+
+
+GAUGE_REL_EPS = 1e-12       # relative perturbation of the sector coordinates (gauge check)
+GAUGE_TOL = 1e-9            # penalty change that flags RYD_STATUS_GAUGE_UNSTABLE
+GAUGE_COPIES = 6
+
+
+def mixed_phase(state: np.ndarray, n: int, dim: int = 3, gauge_check: bool = True,
+                n_threads: int = 0, rel_eps: float = GAUGE_REL_EPS, tol: float = GAUGE_TOL,
+                copies: int = GAUGE_COPIES) -> Tuple[np.ndarray, np.ndarray]:
+    """The reference's mixed-state controlled phase (RG/simulation.py:424-452) for every
+    point of a Lindblad state block (sector rows, >= 4n columns), through the C-ABI host
+    epilogue ryd_mixed_phase on scipy's own LAPACK zheevr (so each phase equals
+    scipy.linalg.eigh's -- QuTiP 5's eigensolver -- on the same rho).  Returns
+    (phases[n, 4], flags[n]): phi_x = np.angle(<x|v_max>) exactly as the reference forms
+    it, and RYD_STATUS_GAUGE_UNSTABLE where the penalty is not a function of rho at
+    relative precision rel_eps."""
+    lib = N.load()
+    if n_threads <= 0:          # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() shows more)
+        n_threads = int(os.environ.get("RYD_HOST_THREADS", min(16, os.cpu_count() or 1)))
+    st = np.ascontiguousarray(state, dtype=np.float64)
+    out = np.zeros((N.MP_WIDTH, max(n, 1)), dtype=np.float64)
+    flags = np.zeros(max(n, 1), dtype=np.uint32)
+    dptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    N.check(lib.ryd_mixed_phase(N.scipy_zheevr(), dim, dptr(st), n, st.shape[1],
+                                copies if gauge_check else 0, rel_eps, tol, n_threads,
+                                dptr(out), out.shape[1], flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+    v = out[N.MP["V0"]:N.MP["V0"] + 8:2, :n] + 1j * out[N.MP["V0"] + 1:N.MP["V0"] + 8:2, :n]
+    return np.angle(v).T.copy(), flags[:n]
 
 
 @dataclass

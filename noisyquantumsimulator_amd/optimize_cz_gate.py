@@ -357,7 +357,7 @@ def default_batch_evaluator(simulation_inputs, n: int, include_noise: bool, over
                                     overrides=overrides, **apparatus)
     m = extract_metrics_batch(br)
     m["_batch"] = br.batch
-    return m, br.status == 0
+    return m, br.ok
 
 
 def _evaluate_rows(evaluator, si, X_over: Dict[str, Any], n: int, include_noise: bool, apparatus_rows):

@@ -30,6 +30,8 @@ from typing import Any, Dict, Optional, Sequence
 import numpy as np
 
 from . import protocols as P
+from ._native import (STATUS_DARK_STATE_SIGN, STATUS_OMEGA_RANGE,
+                      STATUS_WEAK_BLOCKADE)
 from . import species as S
 from .constants import C, EPS0, HBAR, KB, MU_B
 
@@ -151,6 +153,7 @@ class DerivedBatch:
     bangbang_phases: Optional[np.ndarray] = None    # (n, nseg)
     warnings: list = field(default_factory=list)
     noise_config: Any = None                        # the NoiseSourceConfig the points share
+    status_bits: Optional[np.ndarray] = None        # (n,) RYD_STATUS_* warning bits per point
 
     def __getitem__(self, k):
         return self.cols[k]
@@ -367,6 +370,10 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
 
     Om = cols["Omega"]
     cols["V_over_Omega"] = np.where(Om > 0, cols["V"] / np.where(Om > 0, Om, 1.0), np.inf)
+    # the reference's UserWarnings, per point (include/ryd_engine.h RYD_STATUS_* warning bits)
+    bits = np.zeros(n, dtype=np.uint32)
+    om_range = (Om > 2 * np.pi * 100e6) | (Om < 2 * np.pi * 0.1e6)      # RG/simulation.py:2930-2946
+    bits[om_range] |= STATUS_OMEGA_RANGE
     if np.any(Om > 2 * np.pi * 100e6):
         flags.append("omega_above_physical_limit")
         warnings.warn("Ω/2π exceeds physical limit (~100 MHz). Results may be unphysical.",
@@ -375,9 +382,12 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
         flags.append("omega_very_low")
         warnings.warn("Ω/2π is very low. Gate will be very slow and susceptible to decoherence.",
                       UserWarning)
-    if protocol == "levine_pichler" and np.any(cols["V_over_Omega"] < 10):
-        flags.append("weak_blockade")
-        warnings.warn("V/Ω < 10. Blockade too weak for reliable CZ gate!", UserWarning)
+    if protocol == "levine_pichler":              # get_adaptive_protocol_params (RG/protocols.py:615-619)
+        weak = cols["V_over_Omega"] < 10
+        bits[weak] |= STATUS_WEAK_BLOCKADE
+        if np.any(weak):
+            flags.append("weak_blockade")
+            warnings.warn("V/Ω < 10. Blockade too weak for reliable CZ gate!", UserWarning)
 
     # LP: second-pulse phase factor (RG/simulation.py:3192)
     if protocol == "levine_pichler":
@@ -401,7 +411,24 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
         raw = ov.get("delta_over_omega", si.delta_over_omega)
         mag = np.abs(_bc(raw if raw is not None else d["delta_over_omega"], n))
         sdom = np.where(Delta_e > 0, -mag, mag)
+        if "smooth_delta_over_omega" in ov:      # ABI-level override of the signed value
+            sdom = _bc(ov["smooth_delta_over_omega"], n).astype(float)
         cols["smooth_delta_over_omega"] = sdom
+        # evolve_smooth_sinusoidal_jp's checks (RG/simulation.py:1631-1647, :1670-1676)
+        dark_ok = np.where(Delta_e > 0, sdom < 0, sdom > 0)
+        dark_bad = ~dark_ok & (sdom != 0)
+        bits[dark_bad] |= STATUS_DARK_STATE_SIGN
+        if np.any(dark_bad):
+            flags.append("dark_state_sign")
+            warnings.warn("Dark state condition violated! The two-photon detuning has the wrong sign "
+                          "for the intermediate-state detuning. This will increase scattering error.",
+                          UserWarning)
+        weak = cols["V_over_Omega"] < 5
+        bits[weak] |= STATUS_WEAK_BLOCKADE
+        if np.any(weak):
+            flags.append("weak_blockade")
+            warnings.warn("V/Ω may be too weak for reliable CZ operation. Recommend V/Ω > 10 for "
+                          "high-fidelity gates.", UserWarning)
         cols["Delta_seg"] = sdom * Om
         otv = ov.get("omega_tau", si.omega_tau)
         cols["tau_total"] = _bc(otv if otv is not None else d["omega_tau"], n) / Om
@@ -458,7 +485,7 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
     return DerivedBatch(protocol=protocol, pulse_shape=pulse_shape, dim=hilbert_space_dim,
                         include_noise=include_noise, trap_laser_on=trap_laser_on, n=n, cols=cols,
                         bangbang_times=bb_t, bangbang_phases=bb_p, warnings=flags,
-                        noise_config=noise)
+                        noise_config=noise, status_bits=bits)
 
 
 def area_correction_factor(pulse_shape: str, tau) -> np.ndarray:

@@ -14,13 +14,19 @@ phases, controlled phase, cos^2 penalty, average) comes from the GPU summary.
 Noisy (rho) points: populations come from the GPU; the reference's controlled
 phase uses the dominant eigenvector of each 9x9 rho (:424-452), whose phase is
 the eigensolver's gauge choice (SURVEY.md §7 hard part 3).  ``phase_penalty``:
-  "reference" (default) -- LAPACK eigh on the host on the full rho, as QuTiP's
-                 Qobj.eigenstates does (scipy.linalg.eigh by default,
-                 ``eigh="numpy"`` for numpy's batched zheevd);
+  "reference" (default) -- the C-ABI host epilogue ryd_mixed_phase: LAPACK zheevr
+                 (scipy's own, QuTiP 5's eigensolver) on every rho, threaded, phases
+                 bit-identical to scipy.linalg.eigh + np.angle; with ``gauge_check``
+                 each point whose penalty is not a function of rho at 1e-12 relative
+                 precision gets RYD_STATUS_GAUGE_UNSTABLE.
+                 ``eigh="numpy"`` or a callable: the per-matrix Python path instead;
   "none"       -- gauge-invariant population fidelity only (F11 unpenalised).
+Status bits per point: kernel failures (RYD_STATUS_FAIL_MASK) plus the reference's
+warnings (weak blockade, dark-state sign, Omega range) and the gauge flag.
 """
 from __future__ import annotations
 
+import math
 import warnings
 from dataclasses import dataclass, field
 from types import SimpleNamespace
@@ -142,6 +148,18 @@ def compute_CZ_fidelity(results: Dict[str, np.ndarray], extract_global_phase: bo
     return fid, float(np.mean([fid[k] for k in LABELS])), phase_info
 
 
+def _cp_penalty(ph: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """(controlled phase, penalty) from phases ph[n, 4] (00, 01, 10, 11), with the
+    reference's operation order (RG/simulation.py:444-452)."""
+    cp = ph[:, 3] - ph[:, 1] - ph[:, 2] + ph[:, 0]
+    cp = (cp + np.pi) % (2 * np.pi) - np.pi
+    err = np.minimum(np.abs(cp - np.pi), np.abs(cp + np.pi))
+    # the reference squares a numpy scalar: np.float64 ** 2 is libm pow(x, 2.0), which
+    # differs from x * x (numpy's vectorised ** 2) in the last bit for ~0.1% of inputs
+    c = np.cos(err / 2).tolist()
+    return cp, np.fromiter((math.pow(v, 2.0) for v in c), dtype=np.float64, count=len(c))
+
+
 def mixed_phase_penalty(rho: np.ndarray, eigh=None) -> Tuple[np.ndarray, np.ndarray]:
     """Vectorised dominant-eigenvector controlled phase for rho[n, 4, D, D] (D = 9 or 16)
     -> (controlled_phase[n], penalty[n])."""
@@ -261,6 +279,15 @@ class BatchResult:
     def n(self):
         return self.batch.n
 
+    @property
+    def ok(self) -> np.ndarray:
+        """Points the engine evolved without failure (warning bits do not count)."""
+        return (self.status & N.STATUS_FAIL_MASK) == 0
+
+    @property
+    def gauge_unstable(self) -> np.ndarray:
+        return (self.status & N.STATUS_GAUGE_UNSTABLE) != 0
+
     def __len__(self):
         return self.n
 
@@ -290,7 +317,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                            include_noise: bool = True, background_loss_rate_hz=None,
                            trap_laser_on: bool = True, overrides: Optional[Dict[str, Any]] = None,
                            phase_penalty: str = "reference", eigh=None, return_states: bool = False,
-                           devices=None, method: str = "chebyshev") -> BatchResult:
+                           devices=None, method: str = "chebyshev", gauge_check: bool = True) -> BatchResult:
     """Evaluate many simulate_CZ_gate points in one GPU pass (see module doc)."""
     if hilbert_space_dim not in (3, 4):
         raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
@@ -315,7 +342,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     pops = np.zeros((nn, 4))
     cp = np.full(nn, np.nan)
     pen = np.ones(nn)
-    status = np.zeros(nn, np.uint32)
+    status = b.status_bits.copy() if b.status_bits is not None else np.zeros(nn, np.uint32)
     states = None
     if return_states:
         states = {"ket": np.zeros((nn, 4, D), complex), "rho": np.zeros((nn, 4, D, D), complex)}
@@ -328,7 +355,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
         r = eng.run(E.pack_params(b, idx), key, evol, shape=shape,
                     method=method if dim == 3 else "chebyshev", dim=dim)
         kms += r.kernel_ms
-        status[idx] = r.status
+        status[idx] |= r.status
         P = r.populations()
         pops[idx] = P
         if evol == "ket":
@@ -337,12 +364,17 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
             if return_states:
                 states["ket"][idx] = r.kets()
         else:
-            need_rho = return_states or phase_penalty == "reference"
+            host_eigh = phase_penalty == "reference" and eigh not in (None, "scipy")
+            if phase_penalty == "reference" and not host_eigh:
+                ph, gflags = E.mixed_phase(r.state, idx.size, dim, gauge_check=gauge_check)
+                cp[idx], pen[idx] = _cp_penalty(ph)
+                status[idx] |= gflags
+            need_rho = return_states or host_eigh
             if need_rho:
                 for s0 in range(0, idx.size, 65536):
                     sl = slice(s0, s0 + 65536)
                     rho = E.expand_rho(r.state[:, 4 * s0:4 * (s0 + 65536)], min(65536, idx.size - s0), dim)
-                    if phase_penalty == "reference":
+                    if host_eigh:
                         c_, p_ = mixed_phase_penalty(rho, eigh)
                         cp[idx[sl]], pen[idx[sl]] = c_, p_
                     if return_states:
@@ -415,7 +447,7 @@ def simulate_CZ_gate(
         NA=NA, spacing_factor=spacing_factor, include_noise=include_noise,
         background_loss_rate_hz=background_loss_rate_hz, trap_laser_on=trap_laser_on,
         phase_penalty="reference", eigh=eigh, return_states=True)
-    if br.status[0] != 0:
+    if not br.ok[0]:
         raise RuntimeError(f"GPU engine failed for this point (status bits {int(br.status[0])})")
     b = br.batch
     c = {k: (v[0] if np.ndim(v) > 0 else v) for k, v in b.cols.items()}

@@ -35,6 +35,11 @@ Two integrators are provided for every segment:
 Parity pins (tests/test_oracle_golden.py): the published noise-free fidelities
 of the reference notebooks and the closed-form decay
 known-answer test of scripts/archive/test_mesolve_direct.py:34-51.
+
+Mixed-state phase penalty: ``cz_fidelity(..., eigh=scipy.linalg.eigh)`` is the
+reference's procedure (QuTiP 5's eigensolver); ``snap_structural_zeros`` gives the
+exact zeros QuTiP's integration keeps; ``gauge_unstable`` tells whether the penalty
+is a function of rho at 1e-12 relative precision (mostly it is not).
 """
 from __future__ import annotations
 
@@ -399,6 +404,55 @@ def cz_fidelity(results: Dict[str, np.ndarray], dim: int = 3,
     info["F11_with_phase"] = fid["11"]
     avg = float(np.mean([fid[k] for k in LABELS]))
     return fid, avg, info
+
+
+def structural_support(dim: int = 3) -> np.ndarray:
+    """Boolean D x D mask of the rho entries the four basis inputs can ever populate.
+    H and every c_op conserve each atom's {1, r}-excitation number, so an output rho_x
+    lives on e_i (x) e_j with e = {|0><0|, |1><1|, |r><r|, |1><r|, |r><1|} (dim 4: +
+    |r-><r-|); everything else is exactly zero in QuTiP's sparse ZVODE integration."""
+    single = np.zeros((dim, dim), dtype=bool)
+    single[0, 0] = single[1, 1] = single[2, 2] = single[1, 2] = single[2, 1] = True
+    if dim == 4:
+        single[3, 3] = True
+    return np.kron(single, single)
+
+
+def snap_structural_zeros(rho: np.ndarray, dim: int = 3) -> np.ndarray:
+    """rho with the entries outside structural_support set to exactly +0.0 (the dense
+    expm propagator leaves ~1e-17 residues there; QuTiP's output has exact zeros)."""
+    out = np.array(rho, dtype=complex, copy=True)
+    out[~structural_support(dim)] = 0.0
+    return out
+
+
+def gauge_unstable(results: Dict[str, np.ndarray], dim: int = 3, rel_eps: float = 1e-12,
+                   copies: int = 6, tol: float = 1e-9, seed: int = 7) -> Tuple[bool, float]:
+    """Does the reference's mixed-state penalty (cz_fidelity with scipy.linalg.eigh, the
+    eigensolver QuTiP 5 uses) stay put when every nonzero entry of each rho is scaled by
+    (1 +- rel_eps)?  Hermitian sign patterns: copy 1 all +, copy 2 all -, then random.
+    Returns (unstable, max |penalty change|).  The LAPACK eigenvector phase is decided
+    by rounding residues in the Householder reduction, so for most noisy points it is
+    not."""
+    eigh = lambda m: sla.eigh(m)
+    _, _, info0 = cz_fidelity(results, dim, eigh=eigh)
+    rng = np.random.default_rng(seed)
+    spread = 0.0
+    for c in range(copies):
+        pert = {}
+        for lab, rho in results.items():
+            D = rho.shape[0]
+            if c == 0:
+                sgn = np.ones((D, D))
+            elif c == 1:
+                sgn = -np.ones((D, D))
+            else:
+                u = rng.choice([-1.0, 1.0], size=(D, D))
+                sgn = np.triu(u) + np.triu(u, 1).T
+            pert[lab] = rho * (1.0 + rel_eps * sgn)
+        _, _, info = cz_fidelity(pert, dim, eigh=eigh)
+        spread = max(spread, abs(info["cz_phase_fidelity"] - info0["cz_phase_fidelity"]))
+    return spread > tol, spread
 
 
 def decay_kat(gamma: float, t: np.ndarray, method: str = "expm") -> np.ndarray:

@@ -14,6 +14,9 @@ What it does
 3. Evolves the App-B / parity configurations with the expm oracle
    (oracle/lindblad_oracle.py) and records final states + fidelities, together
    with the reference notebooks' PUBLISHED numbers -> evolution_golden.json.
+   Noisy states get QuTiP's exact structural zeros (snap_structural_zeros), their
+   reference avg_fidelity uses scipy.linalg.eigh (QuTiP 5's eigensolver), and each
+   records whether that penalty is a function of rho at 1e-12 (gauge_unstable).
 
 Nothing here is shipped; the GPU box only sees the JSON fixtures.
 """
@@ -340,13 +343,22 @@ def main():
         d = ref_derive(R, cfg)
         p = point_spec(R, cfg, d)
         res = O.run_point(p, method="expm")
-        fid, avg, info = O.cz_fidelity(res)
+        unstable, spread = False, 0.0
+        if cfg.get("include_noise", True):
+            # QuTiP keeps the structural zeros exact; the reference's eigensolver is
+            # scipy.linalg.eigh (QuTiP 5 Qobj.eigenstates)
+            res = {k: O.snap_structural_zeros(v, cfg.get("dim", 3)) for k, v in res.items()}
+            unstable, spread = O.gauge_unstable(res, cfg.get("dim", 3))
+        import scipy.linalg as sla
+        fid, avg, info = O.cz_fidelity(res, eigh=lambda m: sla.eigh(m))
         states = {k: (np.stack([v.real, v.imag]).tolist()) for k, v in res.items()}
         evo.append(dict(name=cfg["name"], config=cfg, derived=d, states=states, fidelities=fid,
                         avg_fidelity=avg, phase_info={k: v for k, v in info.items()},
+                        gauge_unstable=bool(unstable), gauge_spread=float(spread),
                         published=PUBLISHED.get(cfg["name"], {})))
         print(f"{cfg['name']:28s} avg={avg:.8f} F11={fid['11']:.8f} "
-              f"pen={info['cz_phase_fidelity']:.6f} perr={info['phase_error_from_pi_deg']:.2f}")
+              f"pen={info['cz_phase_fidelity']:.6f} perr={info['phase_error_from_pi_deg']:.2f} "
+              f"gauge_unstable={unstable} spread={spread:.3g}")
     # App B row 5 (examples/neutral_atoms_rydberg_cz_gate.ipynb:10294-10299): notebook-local
     # two-pulse LP, kets, no light shifts, Omega = 2 pi 1 MHz, V/Omega = 100
     Om = 2 * np.pi * 1e6

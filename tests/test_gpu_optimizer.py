@@ -8,7 +8,9 @@ import pytest
 
 import oracle_evaluator as OE
 from noisyquantumsimulator_amd import optimization as OPT
-from noisyquantumsimulator_amd import optimize_cz_gate as OC
+import importlib
+
+OC = importlib.import_module("noisyquantumsimulator_amd.optimize_cz_gate")   # the package exports the function of the same name
 from noisyquantumsimulator_amd import simulation as SIM
 
 pytestmark = pytest.mark.gpu

@@ -10,7 +10,9 @@ from scipy.optimize import differential_evolution
 
 import oracle_evaluator as OE
 from noisyquantumsimulator_amd import configurations as CF
-from noisyquantumsimulator_amd import optimize_cz_gate as OC
+import importlib
+
+OC = importlib.import_module("noisyquantumsimulator_amd.optimize_cz_gate")   # the package exports the function of the same name
 from noisyquantumsimulator_amd import physics as PH
 
 
