@@ -312,9 +312,10 @@ int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* de
  * pi| (:444-452).  Output: the component <x|v_max> per input (the phase is its angle).  `zheevr` is the caller's LAPACK zheevr (Fortran ABI, 32-bit ints;
  * the Python layer passes scipy's, so the phases equal scipy.linalg.eigh's bit for
  * bit).  `state` = Lindblad sector rows as ryd_run_batch writes them ([25 | 36][ld]).
- * Gauge check: the same procedure on n_perturb copies with every sector coordinate
- * scaled by (1 +- rel_eps); out_flags[i] |= RYD_STATUS_GAUGE_UNSTABLE if any penalty
- * moves by more than tol.  Host only, n_threads worker threads (0 = all cores). */
+ * Gauge check: the same procedure on up to n_perturb copies of each rho with the real
+ * and imaginary parts of every lower-triangle entry scaled independently by (1 +-
+ * rel_eps) (deterministic sign patterns); out_flags[i] |= RYD_STATUS_GAUGE_UNSTABLE as
+ * soon as a penalty moves by more than tol.  Host only, n_threads worker threads (0 = all cores). */
 #define RYD_MP_V0       0   /* <x|v_max> as (re, im) row pairs, x = 00, 01, 10, 11; the
                                phase is its angle (taken by the caller: the reference
                                uses np.angle)                                       */

@@ -56,7 +56,7 @@ def expand_ket(state: np.ndarray, n: int, dim: int = 3) -> np.ndarray:
 
 GAUGE_REL_EPS = 1e-12       # relative perturbation of the sector coordinates (gauge check)
 GAUGE_TOL = 1e-9            # penalty change that flags RYD_STATUS_GAUGE_UNSTABLE
-GAUGE_COPIES = 6
+GAUGE_COPIES = 16          # probes (an unstable point usually stops after a few); see ryd_mixed_phase
 
 
 def mixed_phase(state: np.ndarray, n: int, dim: int = 3, gauge_check: bool = True,

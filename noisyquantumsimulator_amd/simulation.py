@@ -317,7 +317,8 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                            include_noise: bool = True, background_loss_rate_hz=None,
                            trap_laser_on: bool = True, overrides: Optional[Dict[str, Any]] = None,
                            phase_penalty: str = "reference", eigh=None, return_states: bool = False,
-                           devices=None, method: str = "chebyshev", gauge_check: bool = True) -> BatchResult:
+                           devices=None, method: str = "chebyshev", gauge_check: bool = True,
+                           gauge_copies: Optional[int] = None) -> BatchResult:
     """Evaluate many simulate_CZ_gate points in one GPU pass (see module doc)."""
     if hilbert_space_dim not in (3, 4):
         raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
@@ -366,7 +367,8 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
         else:
             host_eigh = phase_penalty == "reference" and eigh not in (None, "scipy")
             if phase_penalty == "reference" and not host_eigh:
-                ph, gflags = E.mixed_phase(r.state, idx.size, dim, gauge_check=gauge_check)
+                ph, gflags = E.mixed_phase(r.state, idx.size, dim, gauge_check=gauge_check,
+                                           copies=gauge_copies if gauge_copies is not None else E.GAUGE_COPIES)
                 cp[idx], pen[idx] = _cp_penalty(ph)
                 status[idx] |= gflags
             need_rho = return_states or host_eigh

@@ -427,13 +427,14 @@ def snap_structural_zeros(rho: np.ndarray, dim: int = 3) -> np.ndarray:
 
 
 def gauge_unstable(results: Dict[str, np.ndarray], dim: int = 3, rel_eps: float = 1e-12,
-                   copies: int = 6, tol: float = 1e-9, seed: int = 7) -> Tuple[bool, float]:
+                   copies: int = 64, tol: float = 1e-9, seed: int = 7) -> Tuple[bool, float]:
     """Does the reference's mixed-state penalty (cz_fidelity with scipy.linalg.eigh, the
-    eigensolver QuTiP 5 uses) stay put when every nonzero entry of each rho is scaled by
-    (1 +- rel_eps)?  Hermitian sign patterns: copy 1 all +, copy 2 all -, then random.
-    Returns (unstable, max |penalty change|).  The LAPACK eigenvector phase is decided
-    by rounding residues in the Householder reduction, so for most noisy points it is
-    not."""
+    eigensolver QuTiP 5 uses) stay put when the real and imaginary parts of every entry
+    of each rho's lower triangle (what LAPACK reads) are scaled independently by
+    (1 +- rel_eps)?  Copy 1 all +, copy 2 all -, then random sign patterns.  Returns
+    (unstable, max |penalty change|).  The LAPACK eigenvector phase is decided by
+    rounding in the Householder reduction and the tridiagonal eigenvector
+    normalisation, so for most noisy points it is not."""
     eigh = lambda m: sla.eigh(m)
     _, _, info0 = cz_fidelity(results, dim, eigh=eigh)
     rng = np.random.default_rng(seed)
@@ -442,14 +443,13 @@ def gauge_unstable(results: Dict[str, np.ndarray], dim: int = 3, rel_eps: float 
         pert = {}
         for lab, rho in results.items():
             D = rho.shape[0]
-            if c == 0:
-                sgn = np.ones((D, D))
-            elif c == 1:
-                sgn = -np.ones((D, D))
+            if c < 2:
+                s1 = s2 = np.full((D, D), 1.0 if c == 0 else -1.0)
             else:
-                u = rng.choice([-1.0, 1.0], size=(D, D))
-                sgn = np.triu(u) + np.triu(u, 1).T
-            pert[lab] = rho * (1.0 + rel_eps * sgn)
+                s1 = rng.choice([-1.0, 1.0], size=(D, D))
+                s2 = rng.choice([-1.0, 1.0], size=(D, D))
+            q = rho.real * (1.0 + rel_eps * s1) + 1j * rho.imag * (1.0 + rel_eps * s2)
+            pert[lab] = np.tril(q) + np.tril(q, -1).conj().T
         _, _, info = cz_fidelity(pert, dim, eigh=eigh)
         spread = max(spread, abs(info["cz_phase_fidelity"] - info0["cz_phase_fidelity"]))
     return spread > tol, spread

@@ -10,6 +10,14 @@ if REPO not in sys.path:
     sys.path.insert(0, REPO)
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# The oracle works on 81 x 81 (at most 729 x 729) matrices: threaded BLAS only thrashes
+# there (a 16-thread OpenBLAS made one smooth-JP oracle point ~20x slower).
+try:
+    from threadpoolctl import threadpool_limits
+    _BLAS_LIMIT = threadpool_limits(1)
+except ImportError:                                       # pragma: no cover
+    _BLAS_LIMIT = None
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
