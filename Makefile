@@ -10,7 +10,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -Wno-unuse
 all: $(SO)
 
 $(SO): $(SRC) $(PKG)/csrc/ryd_traj.inc $(PKG)/csrc/ryd_sym16.inc $(PKG)/csrc/ryd_epilogue.inc include/ryd_engine.h
-	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC)
+	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC) -ldl
 
 resource-usage: $(SRC)
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -o /tmp/ryd_ru.so $(SRC) 2>&1 | \

@@ -101,7 +101,43 @@ def cpu_baseline(sample: int, procs: int, workload: str = "c2"):
     out = subprocess.run([sys.executable, "-m", "oracle.cpu_baseline", "--sample", str(sample),
                           "--procs", str(procs), "--workload", workload], cwd=REPO, env=env, check=True,
                          capture_output=True, text=True, timeout=600)
-    return json.loads(out.stdout.strip().splitlines()[-1])
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    # `cores` = worker processes actually used; the box's visible CPUs beside it
+    res["host_cpus_visible"] = os.cpu_count()
+    res["cpu_share"] = ("one-GPU box share: OMP_NUM_THREADS=" + os.environ.get("OMP_NUM_THREADS", "?")
+                        + "; os.cpu_count() counts the whole machine")
+    res["per_core"] = res["value"] / max(1, res["cores"])
+    return res
+
+
+def cpu_procs() -> int:
+    """Worker processes for the CPU baseline: the CPU share of this box
+    (OMP_NUM_THREADS, 16 on the GPU box), capped by the visible CPUs."""
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(share, os.cpu_count() or 1))
+
+
+def end_to_end_c2():
+    """simulate_CZ_gate_batch on the C2 grid: derivation (host) + engine (host-buffer
+    boundary) + the reference-penalty epilogue (zheevr on host threads, 16-probe gauge
+    check) -- the whole Python drop-in call, wall clock, second of two calls."""
+    from noisyquantumsimulator_amd import simulation as S
+    from noisyquantumsimulator_amd import sweeps as SW
+    si, n, kw = SW.omega_delta_call()
+    out = {}
+    for gauge in (True, False):
+        for _ in range(2):
+            t0 = time.perf_counter()
+            br = S.simulate_CZ_gate_batch(si, n, gauge_check=gauge, **kw)
+            dt = time.perf_counter() - t0
+        assert br.ok.all()
+        key = "gauge_check" if gauge else "no_gauge_check"
+        out[key] = dict(points_per_s=n / dt, wall_ms=dt * 1e3,
+                        **{k: round(v, 3) for k, v in br.timings.items()},
+                        gauge_unstable=int(br.gauge_unstable.sum()))
+    out["points"] = n
+    out["call"] = "simulate_CZ_gate_batch(LPSimulationInputs(medium), 10000, overrides=C2 grid)"
+    return out
 
 
 # C5 (three-atom trajectories) accounting, per include/ryd_engine.h RYD_TS_*:
@@ -172,7 +208,7 @@ def run_c5(args, ws, rank, local, pg):
                          "bytes_per_launch": C5_BYTES_PER_POINT * n},
     }
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        procs = max(1, min(16, os.cpu_count() or 1))
+        procs = cpu_procs()
         out["cpu_baseline"] = cpu_baseline(min(args.cpu_sample, 64), procs, "c5")
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -269,9 +305,21 @@ def main():
     rh = eng.run(params, protocol, "lindblad", n_steps=n_steps, method=args.method)
     t_h = time.perf_counter() - t_h
     assert np.all(rh.status == 0)
+    # second call: the handle's device workspace and pinned staging are warm
+    t_h = time.perf_counter()
+    rh = eng.run(params, protocol, "lindblad", n_steps=n_steps, method=args.method)
+    t_h = time.perf_counter() - t_h
+    assert np.all(rh.status == 0)
+    tl = eng.last_timeline()
+    bytes_d2h = 8 * (25 * 4 + E.N.NSUMMARY) * n + 4 * n
     host_path = {"points_per_s": n / t_h, "wall_ms": t_h * 1e3, "h2d_ms": rh.h2d_ms,
-                 "kernel_ms": rh.kernel_ms, "d2h_ms": rh.d2h_ms,
-                 "bytes_d2h": 8 * (25 * 4 + 20) * n + 4 * n}
+                 "kernel_ms": rh.kernel_ms, "d2h_ms": rh.d2h_ms, "bytes_d2h": bytes_d2h,
+                 "d2h_gbs": bytes_d2h / (rh.d2h_ms * 1e-3) / 1e9 if rh.d2h_ms > 0 else None,
+                 "host_pack_ms": tl["pack_ms"], "host_unpack_ms": tl["unpack_ms"],
+                 "staging": "persistent device workspace + pinned staging per handle slot; "
+                            "unpack into the caller's strided numpy arrays on host threads"}
+    if args.workload == "c2" and ws == 1:
+        out_e2e = end_to_end_c2()
     strong = args.workload == "c4"
     global_points = SW.C4_POINTS if strong else n * ws
     total_points = global_points * args.steps
@@ -295,12 +343,13 @@ def main():
                      "traffic": traffic, "kernel_ms": k_ms, "flops_per_launch": flops,
                      "exec_over_useful": res.matvec_exec / max(res.matvec_useful, 1)},
         "host_path": host_path,
+        "end_to_end": out_e2e if args.workload == "c2" and ws == 1 else None,
         "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": bytes_per_point * n},
     }
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        procs = max(1, min(16, os.cpu_count() or 1))
+        procs = cpu_procs()
         # C3 points cost ~6 core-seconds each on the CPU path: a smaller sample
         sample = args.cpu_sample if args.workload != "c3" else min(args.cpu_sample, 32)
         out["cpu_baseline"] = cpu_baseline(sample, procs, args.workload)

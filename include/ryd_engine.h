@@ -327,6 +327,30 @@ int ryd_mixed_phase(void* zheevr, int dim, const double* state, int64_t n, int64
                     int n_perturb, double rel_eps, double tol, int n_threads,
                     double* out, int64_t ld_out, uint32_t* out_flags);
 
+/* Private LAPACK instances for the threaded epilogue.  The pool is ref_zheevr itself
+ * plus up to `copies` - 1 copies of the shared object `path` loaded into fresh link
+ * namespaces (dlmopen), each set to one BLAS
+ * thread (`threads_symbol`, may be NULL), and admits a copy only if its `zheevr_symbol`
+ * reproduces `ref_zheevr` bit for bit on test matrices.  ryd_mixed_phase called with
+ * ref_zheevr then runs one instance per worker thread (min(n_threads, pool size)
+ * threads): OpenBLAS serialises concurrent callers of one instance on a process-wide
+ * lock.  *n_loaded = pool size (loading stops quietly when namespaces or static TLS run
+ * out); an error only if no copy could be loaded. */
+int ryd_lapack_pool(void* ref_zheevr, const char* path, const char* zheevr_symbol,
+                    const char* threads_symbol, int copies, int* n_loaded);
+
+/* Timeline of the handle's last host-buffer call (ryd_run_batch / _coherences /
+ * _trajectories).  Those calls keep a device workspace and a pinned host staging buffer
+ * per slot across calls, enqueue every slot (pack -> H2D -> kernel -> D2H into staging)
+ * before the first wait, then unpack staging into the caller's buffers with host
+ * threads.  out[0] = n_slots, out[1] = host pack ms, out[2] = host unpack ms,
+ * out[3] = call wall ms; then per slot RYD_TL_SLOT doubles: device id, H2D start,
+ * kernel start, kernel end, D2H end (ms, HIP events, relative to the start of the first
+ * slot on the same device), points.  cap >= 4 + RYD_TL_SLOT * n_slots. */
+#define RYD_TL_HEAD 4
+#define RYD_TL_SLOT 6
+int ryd_last_timeline(ryd_handle* h, double* out, int64_t cap);
+
 /* Minimal device-memory plumbing so callers need no other GPU runtime. */
 int ryd_malloc(ryd_handle* h, int slot, size_t bytes, void** d_ptr);
 int ryd_free(ryd_handle* h, int slot, void* d_ptr);

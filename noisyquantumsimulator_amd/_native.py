@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RYD_ENGINE_LIB selects an alternative build of the same library (tuning variants)
@@ -49,11 +50,14 @@ TS = dict(MEAN_JUMPS=0, FRAC_JUMPED=1, MAX_JUMPS=2, TRACE=3, QUBIT_POP=4, ITER_U
           ITER_EXEC=6, NLADDER=7, NSQUARE=8, RESERVED=9)
 T_NSUMMARY = 10
 
+# ryd_last_timeline layout
+TL_HEAD, TL_SLOT = 4, 6
+
 EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary_width",
             "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",
             "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
             "ryd_run_trajectories", "ryd_run_trajectories_device",
-            "ryd_mixed_phase",
+            "ryd_mixed_phase", "ryd_lapack_pool", "ryd_last_timeline",
             "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize")
 
 
@@ -122,6 +126,9 @@ def load() -> ctypes.CDLL:
                                                     ctypes.POINTER(ctypes.c_float)]
         lib.ryd_mixed_phase.argtypes = [vp, ctypes.c_int, dp, i64, i64, ctypes.c_int, ctypes.c_double,
                                         ctypes.c_double, ctypes.c_int, dp, i64, ctypes.POINTER(ctypes.c_uint32)]
+        lib.ryd_last_timeline.argtypes = [vp, dp, i64]
+        lib.ryd_lapack_pool.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_int)]
         lib.ryd_malloc.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]
         lib.ryd_free.argtypes = [vp, ctypes.c_int, vp]
         lib.ryd_memcpy_h2d.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]
@@ -158,3 +165,28 @@ def scipy_zheevr() -> int:
         api.PyCapsule_GetPointer.argtypes = [ctypes.py_object, ctypes.c_char_p]
         _zheevr = api.PyCapsule_GetPointer(cap, api.PyCapsule_GetName(cap))
     return _zheevr
+
+
+_pool_size: Optional[int] = None
+
+
+def scipy_lapack_pool(copies: int) -> int:
+    """Private copies of scipy's OpenBLAS for the threaded epilogue (ryd_lapack_pool):
+    OpenBLAS serialises concurrent zheevr callers on a process-wide lock, each copy in
+    its own link namespace has its own.  Copies are admitted only if bit-identical to
+    scipy_zheevr() on test matrices.  Returns the pool size (0: none could be loaded --
+    the epilogue then runs on scipy's zheevr itself, correct but serialised)."""
+    global _pool_size
+    if _pool_size is not None and _pool_size >= copies:
+        return _pool_size
+    import glob
+    import scipy
+    libs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(scipy.__file__)), "scipy.libs",
+                                         "libscipy_openblas*.so")))
+    got = ctypes.c_int(0)
+    if not libs or load().ryd_lapack_pool(scipy_zheevr(), libs[0].encode(), b"scipy_zheevr_",
+                                          b"scipy_openblas_set_num_threads", copies, ctypes.byref(got)) != 0:
+        _pool_size = 0
+        return 0
+    _pool_size = got.value
+    return _pool_size

@@ -25,12 +25,17 @@
 //    ~300 B in + 800 B out per point.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -38,10 +43,25 @@
 
 #include "../../include/ryd_engine.h"
 
+// Persistent per-slot workspace of the host-buffer entry points: one device buffer and
+// one pinned host staging buffer with the same layout [params | outputs... | status],
+// grown on demand and reused across calls, plus the slot's timing events.
+struct ryd_slot_work {
+  void* dbuf = nullptr;
+  size_t dcap = 0;
+  void* hbuf = nullptr;     // hipHostMalloc (pinned, portable)
+  size_t hcap = 0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ev_ok = false;
+};
+
 // one stream per device slot; defined at global scope (the header's opaque type)
 struct ryd_handle {
   std::vector<int> dev;
   std::vector<hipStream_t> stream;
+  std::vector<ryd_slot_work> work;
+  std::vector<double> timeline;   // ryd_last_timeline
+  std::mutex mu;                  // one host-buffer call at a time per handle
 };
 
 namespace {
@@ -2121,34 +2141,54 @@ bool jp_split_enabled() {
   return !(e && e[0] == '0');
 }
 
+// The jp workspace pool: a private stream-ordered pool per device, kept warm
+// (release threshold = max) without touching the process's default pool.
+hipMemPool_t jp_pool(int dev) {
+  static std::mutex mu;
+  static std::vector<hipMemPool_t> pools;
+  std::lock_guard<std::mutex> lk(mu);
+  if ((int)pools.size() <= dev) pools.resize(dev + 1, nullptr);
+  if (!pools[dev]) {
+    hipMemPoolProps pp;
+    memset(&pp, 0, sizeof(pp));
+    pp.allocType = hipMemAllocationTypePinned;
+    pp.location.type = hipMemLocationTypeDevice;
+    pp.location.id = dev;
+    hipMemPool_t p = nullptr;
+    if (hipMemPoolCreate(&p, &pp) != hipSuccess) return nullptr;
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(p, hipMemPoolAttrReleaseThreshold, &keep);
+    pools[dev] = p;
+  }
+  return pools[dev];
+}
+
 // Smooth JP, propagator method: jp_rows_kernel -> workspace (25 x 25 doubles per
-// point, stream-ordered allocation, pool kept warm) -> jp_frame_kernel.
+// point, from the private pool) -> jp_frame_kernel.
 int launch_jp_split(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, double* ds,
                     int64_t lds, double* dm, int64_t ldm, uint32_t* dstat, hipStream_t stream) {
   const bool sym = (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0;
   const int64_t blocks_a = (n + PPB - 1) / PPB, blocks_b = (n + FPB - 1) / FPB;
   if (blocks_b > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
-  {
-    int dev = 0;
-    HIPCHK(hipGetDevice(&dev));
-    hipMemPool_t pool;
-    HIPCHK(hipDeviceGetDefaultMemPool(&pool, dev));
-    uint64_t keep = UINT64_MAX;
-    HIPCHK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
-  }
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  hipMemPool_t pool = jp_pool(dev);
+  if (!pool) return fail(RYD_ERR_ALLOC, "jp workspace pool creation failed");
   double* W = nullptr;
-  HIPCHK(hipMallocAsync((void**)&W, sizeof(double) * NC * NC * (size_t)n, stream));
+  HIPCHK(hipMallocFromPoolAsync((void**)&W, sizeof(double) * NC * NC * (size_t)n, pool, stream));
   int ns = d->n_steps, sh = d->shape;
   void* args_a[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&W, (void*)&dm, (void*)&ldm,
                     (void*)&dstat, (void*)&ns, (void*)&sh};
   const void* ka = sym ? (const void*)jp_rows_kernel<true> : (const void*)jp_rows_kernel<false>;
-  HIPCHK(hipLaunchKernel(ka, dim3((unsigned)blocks_a), dim3(BLOCK), args_a, 0, stream));
   void* args_b[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&W, (void*)&ds, (void*)&lds,
                     (void*)&dm, (void*)&ldm, (void*)&dstat, (void*)&ns};
   // SYM holds 157 VGPRs (3 waves per SIMD; a 128 budget spills), the 4-output form 127
   const void* kb = sym ? (const void*)jp_frame_kernel<3, true> : (const void*)jp_frame_kernel<4, false>;
-  HIPCHK(hipLaunchKernel(kb, dim3((unsigned)blocks_b), dim3(BLOCK), args_b, 0, stream));
-  HIPCHK(hipFreeAsync(W, stream));
+  hipError_t e = hipLaunchKernel(ka, dim3((unsigned)blocks_a), dim3(BLOCK), args_a, 0, stream);
+  if (e == hipSuccess) e = hipLaunchKernel(kb, dim3((unsigned)blocks_b), dim3(BLOCK), args_b, 0, stream);
+  hipError_t ef = hipFreeAsync(W, stream);          // on the error path too
+  if (e != hipSuccess) return fail(RYD_ERR_HIP, std::string("jp split launch: ") + hipGetErrorString(e));
+  if (ef != hipSuccess) return fail(RYD_ERR_HIP, std::string("jp workspace free: ") + hipGetErrorString(ef));
   return RYD_OK;
 }
 
@@ -2249,6 +2289,28 @@ int validate_coherences(const ryd_batch_desc* d, int64_t n, int64_t ldp, int64_t
   return RYD_OK;
 }
 
+// HIP events around one launch on a caller's stream (the *_device entry points);
+// the destructor releases them on every path.
+struct LaunchTimer {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int start(hipStream_t s) {
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, s));
+    return RYD_OK;
+  }
+  int stop(hipStream_t s, float* ms) {
+    HIPCHK(hipEventRecord(e1, s));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(ms, e0, e1));
+    return RYD_OK;
+  }
+  ~LaunchTimer() {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+};
+
 // One output array of a partitioned run: `rows` rows of `per_point` doubles per point.
 struct HostOut {
   double* host;
@@ -2257,110 +2319,252 @@ struct HostOut {
   int per_point;
 };
 
-// Range-partition n points over the handle's devices (point i -> device
-// floor(nd*i/n)), one stream each, no inter-device traffic:
-// gather params, run `launch_fn(dp, cnt, ldp, dev_outs, dstat, stream)`, scatter
-// outputs, wait for all.  Device times are the max over devices.
+// Host worker threads for staging copies: RYD_HOST_THREADS, else min(16, cores).
+int host_threads() {
+  const char* e = getenv("RYD_HOST_THREADS");
+  int t = e ? atoi(e) : 0;
+  if (t <= 0) t = std::min(16, (int)std::max(1u, std::thread::hardware_concurrency()));
+  return t;
+}
+
+struct CopyTask {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+
+// memcpy a task list with up to host_threads() threads (serial below 1 MiB); rows
+// larger than 256 KiB are cut so the threads balance.
+void parallel_copy(const std::vector<CopyTask>& in) {
+  std::vector<CopyTask> tasks;
+  size_t total = 0;
+  const size_t cut = 256 << 10;
+  for (const CopyTask& t : in) {
+    total += t.bytes;
+    for (size_t o = 0; o < t.bytes; o += cut)
+      tasks.push_back({(char*)t.dst + o, (const char*)t.src + o, std::min(cut, t.bytes - o)});
+  }
+  int nt = std::min<int64_t>(host_threads(), (int64_t)tasks.size());
+  if (total < (1u << 20) || nt <= 1) {
+    for (const CopyTask& t : tasks) memcpy(t.dst, t.src, t.bytes);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t i; (i = next.fetch_add(1)) < tasks.size();) memcpy(tasks[i].dst, tasks[i].src, tasks[i].bytes);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+}
+
+double host_ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Grow slot k's device + pinned buffers to `bytes` and create its events (once).
+int ensure_slot_work(ryd_handle* h, int k, size_t bytes) {
+  ryd_slot_work& w = h->work[k];
+  if (!w.ev_ok) {
+    for (int j = 0; j < 4; ++j)
+      if (!w.ev[j]) HIPCHK(hipEventCreate(&w.ev[j]));
+    w.ev_ok = true;
+  }
+  if (w.dcap < bytes) {
+    if (w.dbuf) HIPCHK(hipFree(w.dbuf));
+    w.dbuf = nullptr;
+    w.dcap = 0;
+    const size_t cap = align256(bytes + bytes / 4);
+    if (hipMalloc(&w.dbuf, cap) != hipSuccess) {
+      w.dbuf = nullptr;
+      return fail(RYD_ERR_ALLOC, "device workspace allocation failed");
+    }
+    w.dcap = cap;
+  }
+  if (w.hcap < bytes) {
+    if (w.hbuf) HIPCHK(hipHostFree(w.hbuf));
+    w.hbuf = nullptr;
+    w.hcap = 0;
+    const size_t cap = align256(bytes + bytes / 4);
+    if (hipHostMalloc(&w.hbuf, cap, hipHostMallocPortable) != hipSuccess) {
+      w.hbuf = nullptr;
+      return fail(RYD_ERR_ALLOC, "pinned staging allocation failed");
+    }
+    w.hcap = cap;
+  }
+  return RYD_OK;
+}
+
+void release_slot_work(ryd_slot_work& w) {
+  if (w.dbuf) (void)hipFree(w.dbuf);
+  if (w.hbuf) (void)hipHostFree(w.hbuf);
+  for (int j = 0; j < 4; ++j)
+    if (w.ev[j]) (void)hipEventDestroy(w.ev[j]);
+  w = ryd_slot_work();
+}
+
+// Range-partition n points over the handle's devices (point i -> slot
+// floor(nd*i/n)), one stream each, no inter-device traffic.
+// Per slot, in order: pack the shard's parameter columns into the slot's pinned
+// staging buffer, enqueue H2D + `launch_fn(dp, cnt, ldp, off, dev_outs, dstat, stream)`;
+// then every slot's D2H into staging -- all enqueued before the first wait, so devices
+// (and same-device slots) overlap -- then wait slot by slot and unpack staging into
+// the caller's strided buffers with host threads.  Device workspace and staging
+// persist in the handle.  Device times are the max over slots; the per-slot event
+// timeline and the host pack/unpack times go to h->timeline (ryd_last_timeline).
 template <typename LaunchFn>
 int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_params,
                     const std::vector<HostOut>& outs, uint32_t* out_status, LaunchFn launch_fn,
                     double& kms, double& hms, double& dms) {
+  std::lock_guard<std::mutex> lock(h->mu);
+  const auto t_call = std::chrono::steady_clock::now();
   const int nd = (int)h->dev.size();
   const int no = (int)outs.size();
+  if ((int)h->work.size() < nd) h->work.resize(nd);
   struct Part {
     int64_t off, cnt;
-    double* p;
-    std::vector<double*> o;
-    uint32_t* st;
-    hipEvent_t a, b, c, d;
-    bool ev;
+    size_t o_par, o_st;
+    std::vector<size_t> o_out;
+    bool queued;
   };
   std::vector<Part> parts(nd);
-  for (int k = 0; k < nd; ++k) {
-    parts[k].off = n * k / nd;
-    parts[k].cnt = n * (k + 1) / nd - parts[k].off;
-    parts[k].p = nullptr;
-    parts[k].o.assign(no, nullptr);
-    parts[k].st = nullptr;
-    parts[k].ev = false;
-  }
-  auto cleanup = [&]() {
-    for (int k = 0; k < nd; ++k) {
-      Part& P = parts[k];
-      (void)hipSetDevice(h->dev[k]);
-      (void)hipStreamSynchronize(h->stream[k]);
-      if (P.p) (void)hipFree(P.p);
-      for (auto& q : P.o)
-        if (q) (void)hipFree(q);
-      if (P.st) (void)hipFree(P.st);
-      if (P.ev) {
-        (void)hipEventDestroy(P.a);
-        (void)hipEventDestroy(P.b);
-        (void)hipEventDestroy(P.c);
-        (void)hipEventDestroy(P.d);
-      }
-      P.p = nullptr;
-      P.o.assign(no, nullptr);
-      P.st = nullptr;
-      P.ev = false;
-    }
-  };
   kms = hms = dms = 0.0;
+  double pack_ms = 0.0, unpack_ms = 0.0;
+  auto drain = [&](int upto) {   // error path: wait for what was already enqueued
+    for (int k = 0; k < upto; ++k)
+      if (parts[k].queued) {
+        (void)hipSetDevice(h->dev[k]);
+        (void)hipStreamSynchronize(h->stream[k]);
+      }
+  };
   for (int k = 0; k < nd; ++k) {
     Part& P = parts[k];
+    P.off = n * k / nd;
+    P.cnt = n * (k + 1) / nd - P.off;
+    P.queued = false;
     if (P.cnt == 0) continue;
-    (void)hipSetDevice(h->dev[k]);
-    hipStream_t s = h->stream[k];
-    bool ok = hipMalloc(&P.p, sizeof(double) * RYD_NPARAM * P.cnt) == hipSuccess &&
-              hipMalloc(&P.st, sizeof(uint32_t) * P.cnt) == hipSuccess;
-    for (int j = 0; j < no && ok; ++j)
-      ok = hipMalloc(&P.o[j], sizeof(double) * outs[j].rows * outs[j].per_point * P.cnt) == hipSuccess;
-    if (!ok) {
-      cleanup();
-      return fail(RYD_ERR_ALLOC, "device allocation failed");
+    size_t at = 0;
+    P.o_par = at;
+    at = align256(at + sizeof(double) * RYD_NPARAM * P.cnt);
+    P.o_out.resize(no);
+    for (int j = 0; j < no; ++j) {
+      P.o_out[j] = at;
+      at = align256(at + sizeof(double) * outs[j].rows * outs[j].per_point * P.cnt);
     }
-    P.ev = hipEventCreate(&P.a) == hipSuccess && hipEventCreate(&P.b) == hipSuccess &&
-           hipEventCreate(&P.c) == hipSuccess && hipEventCreate(&P.d) == hipSuccess;
-    if (!P.ev) {
-      cleanup();
-      return fail(RYD_ERR_HIP, "event creation failed");
+    P.o_st = at;
+    at = align256(at + sizeof(uint32_t) * P.cnt);
+    hipError_t e = hipSetDevice(h->dev[k]);
+    if (e != hipSuccess) {
+      drain(k);
+      return fail(RYD_ERR_HIP, std::string("set device: ") + hipGetErrorString(e));
     }
-    (void)hipEventRecord(P.a, s);
-    // gather this shard's SoA columns
-    (void)hipMemcpy2DAsync(P.p, sizeof(double) * P.cnt, params + P.off, sizeof(double) * ld_params,
-                           sizeof(double) * P.cnt, RYD_NPARAM, hipMemcpyHostToDevice, s);
-    (void)hipEventRecord(P.b, s);
-    int rc = launch_fn(P.p, P.cnt, P.cnt, P.off, P.o, P.st, s);
+    int rc = ensure_slot_work(h, k, at);
     if (rc) {
-      cleanup();
+      drain(k);
       return rc;
     }
-    (void)hipEventRecord(P.c, s);
-    for (int j = 0; j < no; ++j) {
-      const int64_t w = (int64_t)outs[j].per_point * P.cnt;
-      if (outs[j].rows == 1)       // point-major output: one contiguous slice
-        (void)hipMemcpyAsync(outs[j].host + outs[j].per_point * P.off, P.o[j], sizeof(double) * w,
-                             hipMemcpyDeviceToHost, s);
-      else
-        (void)hipMemcpy2DAsync(outs[j].host + outs[j].per_point * P.off, sizeof(double) * outs[j].ld, P.o[j],
-                               sizeof(double) * w, sizeof(double) * w, outs[j].rows, hipMemcpyDeviceToHost, s);
+    ryd_slot_work& W = h->work[k];
+    char* hb = (char*)W.hbuf;
+    char* db = (char*)W.dbuf;
+    hipStream_t s = h->stream[k];
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<CopyTask> pack;
+    for (int c = 0; c < RYD_NPARAM; ++c)
+      pack.push_back({hb + P.o_par + sizeof(double) * c * P.cnt, params + (int64_t)c * ld_params + P.off,
+                      sizeof(double) * P.cnt});
+    parallel_copy(pack);
+    pack_ms += host_ms_since(t0);
+    std::vector<double*> dout(no);
+    for (int j = 0; j < no; ++j) dout[j] = (double*)(db + P.o_out[j]);
+    e = hipEventRecord(W.ev[0], s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(db + P.o_par, hb + P.o_par, sizeof(double) * RYD_NPARAM * P.cnt,
+                         hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(W.ev[1], s);
+    if (e != hipSuccess) {
+      drain(k);
+      (void)hipStreamSynchronize(s);
+      return fail(RYD_ERR_HIP, std::string("h2d: ") + hipGetErrorString(e));
     }
-    (void)hipMemcpyAsync(out_status + P.off, P.st, sizeof(uint32_t) * P.cnt, hipMemcpyDeviceToHost, s);
-    (void)hipEventRecord(P.d, s);
+    P.queued = true;
+    rc = launch_fn((const double*)(db + P.o_par), P.cnt, P.cnt, P.off, dout, (uint32_t*)(db + P.o_st), s);
+    if (rc) {
+      drain(k + 1);
+      return rc;
+    }
+    e = hipEventRecord(W.ev[2], s);
+    if (e != hipSuccess) {
+      drain(k + 1);
+      return fail(RYD_ERR_HIP, std::string("event: ") + hipGetErrorString(e));
+    }
   }
-  hipError_t err = hipSuccess;
+  // D2Hs only after every slot's H2D: copies of one device's streams share its DMA
+  // rings in submission order, so a D2H (waiting for its kernel) enqueued before the
+  // next slot's H2D would hold that H2D back until the kernel ends.
   for (int k = 0; k < nd; ++k) {
     Part& P = parts[k];
     if (P.cnt == 0) continue;
+    ryd_slot_work& W = h->work[k];
+    (void)hipSetDevice(h->dev[k]);
+    hipStream_t s = h->stream[k];
+    // outputs + status are contiguous in the workspace: one D2H
+    hipError_t e = hipMemcpyAsync((char*)W.hbuf + P.o_out.front(), (char*)W.dbuf + P.o_out.front(),
+                                  P.o_st + sizeof(uint32_t) * P.cnt - P.o_out.front(), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipEventRecord(W.ev[3], s);
+    if (e != hipSuccess) {
+      drain(nd);
+      return fail(RYD_ERR_HIP, std::string("d2h: ") + hipGetErrorString(e));
+    }
+  }
+  hipError_t err = hipSuccess;
+  h->timeline.assign(4 + 6 * (size_t)nd, 0.0);
+  std::vector<hipEvent_t> origin(nd, nullptr);   // first slot's start event, per device
+  for (int k = 0; k < nd; ++k) {
+    Part& P = parts[k];
+    double* tl = &h->timeline[4 + 6 * (size_t)k];
+    tl[0] = h->dev[k];
+    tl[5] = (double)P.cnt;
+    if (P.cnt == 0) continue;
+    ryd_slot_work& W = h->work[k];
     (void)hipSetDevice(h->dev[k]);
     hipError_t e = hipStreamSynchronize(h->stream[k]);
-    if (e != hipSuccess) err = e;
+    if (e != hipSuccess) {
+      err = e;
+      continue;
+    }
     float t;
-    if (hipEventElapsedTime(&t, P.a, P.b) == hipSuccess) hms = fmax(hms, t);
-    if (hipEventElapsedTime(&t, P.b, P.c) == hipSuccess) kms = fmax(kms, t);
-    if (hipEventElapsedTime(&t, P.c, P.d) == hipSuccess) dms = fmax(dms, t);
+    if (hipEventElapsedTime(&t, W.ev[0], W.ev[1]) == hipSuccess) hms = std::max(hms, (double)t);
+    if (hipEventElapsedTime(&t, W.ev[1], W.ev[2]) == hipSuccess) kms = std::max(kms, (double)t);
+    if (hipEventElapsedTime(&t, W.ev[2], W.ev[3]) == hipSuccess) dms = std::max(dms, (double)t);
+    hipEvent_t o = W.ev[0];
+    for (int j = 0; j < k; ++j)
+      if (h->dev[j] == h->dev[k] && parts[j].cnt > 0) {
+        o = h->work[j].ev[0];
+        break;
+      }
+    for (int j = 1; j < 4; ++j)
+      if (hipEventElapsedTime(&t, o, W.ev[j - 1]) == hipSuccess) tl[j] = t;
+    if (hipEventElapsedTime(&t, o, W.ev[3]) == hipSuccess) tl[4] = t;
+    const auto t0 = std::chrono::steady_clock::now();
+    const char* hb = (const char*)W.hbuf;
+    std::vector<CopyTask> unpack;
+    for (int j = 0; j < no; ++j) {
+      const int64_t w = (int64_t)outs[j].per_point * P.cnt;
+      for (int r = 0; r < outs[j].rows; ++r)
+        unpack.push_back({outs[j].host + (int64_t)r * outs[j].ld + (int64_t)outs[j].per_point * P.off,
+                          hb + P.o_out[j] + sizeof(double) * r * w, sizeof(double) * w});
+    }
+    unpack.push_back({out_status + P.off, hb + P.o_st, sizeof(uint32_t) * P.cnt});
+    parallel_copy(unpack);
+    unpack_ms += host_ms_since(t0);
   }
-  cleanup();
+  h->timeline[0] = nd;
+  h->timeline[1] = pack_ms;
+  h->timeline[2] = unpack_ms;
+  h->timeline[3] = host_ms_since(t_call);
   if (err != hipSuccess) return fail(RYD_ERR_HIP, std::string("batch: ") + hipGetErrorString(err));
   return RYD_OK;
 }
@@ -2429,6 +2633,7 @@ int ryd_destroy(ryd_handle* h) {
   for (size_t k = 0; k < h->dev.size(); ++k) {
     (void)hipSetDevice(h->dev[k]);
     (void)hipStreamSynchronize(h->stream[k]);
+    if (k < h->work.size()) release_slot_work(h->work[k]);
     (void)hipStreamDestroy(h->stream[k]);
   }
   delete h;
@@ -2466,6 +2671,15 @@ int ryd_memcpy_d2h(ryd_handle* h, int slot, void* dst, const void* src, size_t b
   return RYD_OK;
 }
 
+int ryd_last_timeline(ryd_handle* h, double* out, int64_t cap) {
+  if (!h || !out) return fail(RYD_ERR_INVALID, "bad args");
+  std::lock_guard<std::mutex> lock(h->mu);
+  if (h->timeline.empty()) return fail(RYD_ERR_INVALID, "no host-buffer call on this handle yet");
+  if (cap < (int64_t)h->timeline.size()) return fail(RYD_ERR_INVALID, "timeline buffer too small");
+  memcpy(out, h->timeline.data(), sizeof(double) * h->timeline.size());
+  return RYD_OK;
+}
+
 int ryd_synchronize(ryd_handle* h) {
   if (!h) return fail(RYD_ERR_INVALID, "handle is NULL");
   for (size_t k = 0; k < h->dev.size(); ++k) {
@@ -2484,22 +2698,14 @@ int ryd_run_batch_device(ryd_handle* h, int slot, const ryd_batch_desc* desc, co
   if (rc) return rc;
   HIPCHK(hipSetDevice(h->dev[slot]));
   hipStream_t s = stream ? (hipStream_t)stream : h->stream[slot];
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  LaunchTimer timer;
   if (elapsed_ms) {
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, s));
+    rc = timer.start(s);
+    if (rc) return rc;
   }
   rc = launch(desc, d_params, n, ld_params, d_state, ld_state, d_summary, ld_summary, d_status, s);
   if (rc) return rc;
-  if (elapsed_ms) {
-    HIPCHK(hipEventRecord(e1, s));
-    HIPCHK(hipEventSynchronize(e1));
-    HIPCHK(hipEventElapsedTime(elapsed_ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-  }
-  return RYD_OK;
+  return elapsed_ms ? timer.stop(s, elapsed_ms) : RYD_OK;
 }
 
 int ryd_run_batch(ryd_handle* h, const ryd_batch_desc* desc, const double* params, int64_t n,
@@ -2615,23 +2821,15 @@ int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* de
     return fail(RYD_ERR_INVALID, "leading dimension too small or negative point_offset");
   HIPCHK(hipSetDevice(h->dev[slot]));
   hipStream_t s = stream ? (hipStream_t)stream : h->stream[slot];
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  LaunchTimer timer;
   if (elapsed_ms) {
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, s));
+    rc = timer.start(s);
+    if (rc) return rc;
   }
   rc = launch_traj(desc, d_params, n, ld_params, point_offset, d_rho, ld_rho, d_se, ld_se, d_summary, ld_summary,
                    d_records, d_status, s);
   if (rc) return rc;
-  if (elapsed_ms) {
-    HIPCHK(hipEventRecord(e1, s));
-    HIPCHK(hipEventSynchronize(e1));
-    HIPCHK(hipEventElapsedTime(elapsed_ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-  }
-  return RYD_OK;
+  return elapsed_ms ? timer.stop(s, elapsed_ms) : RYD_OK;
 }
 
 int ryd_run_coherences_device(ryd_handle* h, int slot, const ryd_batch_desc* desc, const double* d_params,
@@ -2642,22 +2840,14 @@ int ryd_run_coherences_device(ryd_handle* h, int slot, const ryd_batch_desc* des
   if (rc) return rc;
   HIPCHK(hipSetDevice(h->dev[slot]));
   hipStream_t s = stream ? (hipStream_t)stream : h->stream[slot];
-  hipEvent_t e0 = nullptr, e1 = nullptr;
+  LaunchTimer timer;
   if (elapsed_ms) {
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventRecord(e0, s));
+    rc = timer.start(s);
+    if (rc) return rc;
   }
   rc = launch_coherences(desc, d_params, n, ld_params, d_coh, ld_coh, d_status, s);
   if (rc) return rc;
-  if (elapsed_ms) {
-    HIPCHK(hipEventRecord(e1, s));
-    HIPCHK(hipEventSynchronize(e1));
-    HIPCHK(hipEventElapsedTime(elapsed_ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-  }
-  return RYD_OK;
+  return elapsed_ms ? timer.stop(s, elapsed_ms) : RYD_OK;
 }
 
 }  // extern "C"

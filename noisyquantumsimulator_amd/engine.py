@@ -15,7 +15,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import Optional, Sequence, Tuple
+from typing import Any, Dict, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -72,6 +72,8 @@ def mixed_phase(state: np.ndarray, n: int, dim: int = 3, gauge_check: bool = Tru
     lib = N.load()
     if n_threads <= 0:          # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() shows more)
         n_threads = int(os.environ.get("RYD_HOST_THREADS", min(16, os.cpu_count() or 1)))
+    if n_threads > 1 and n >= 64 and os.environ.get("RYD_LAPACK_POOL", "1") != "0":
+        N.scipy_lapack_pool(n_threads)
     st = np.ascontiguousarray(state, dtype=np.float64)
     out = np.zeros((N.MP_WIDTH, max(n, 1)), dtype=np.float64)
     flags = np.zeros(max(n, 1), dtype=np.uint32)
@@ -255,6 +257,19 @@ class Engine:
             status.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(st)))
         return EngineResult(evolution, n, state, summ, status, st.kernel_ms, st.h2d_ms, st.d2h_ms,
                             st.matvec_useful, st.matvec_exec, dim)
+
+    def last_timeline(self) -> Dict[str, Any]:
+        """ryd_last_timeline: host staging times and the per-slot HIP-event timeline of the
+        last host-buffer call (ms; slot times relative to the first slot on its device)."""
+        buf = np.zeros(N.TL_HEAD + N.TL_SLOT * len(self.devices))
+        N.check(self.lib.ryd_last_timeline(self.handle, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                           buf.size))
+        slots = []
+        for k in range(int(buf[0])):
+            t = buf[N.TL_HEAD + N.TL_SLOT * k: N.TL_HEAD + N.TL_SLOT * (k + 1)]
+            slots.append(dict(device=int(t[0]), h2d_start=t[1], kernel_start=t[2], kernel_end=t[3],
+                              d2h_end=t[4], points=int(t[5])))
+        return dict(pack_ms=buf[1], unpack_ms=buf[2], wall_ms=buf[3], slots=slots)
 
     def run_coherences(self, params: np.ndarray, protocol: str, n_steps: Optional[int] = None,
                        shape: str = "square") -> Tuple[np.ndarray, np.ndarray]:

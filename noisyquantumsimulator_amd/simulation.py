@@ -27,6 +27,7 @@ warnings (weak blockade, dark-state sign, Omega range) and the gauge flag.
 from __future__ import annotations
 
 import math
+import time
 import warnings
 from dataclasses import dataclass, field
 from types import SimpleNamespace
@@ -274,6 +275,7 @@ class BatchResult:
     is_mixed: np.ndarray
     states: Optional[np.ndarray] = None   # rho (n,4,9,9) or kets (n,4,9) (complex)
     kernel_ms: float = 0.0
+    timings: Dict[str, float] = field(default_factory=dict)   # host wall ms per stage
 
     @property
     def n(self):
@@ -325,6 +327,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     dim = hilbert_space_dim
     D = dim * dim
     from . import engine as E
+    t_start = time.perf_counter()
     b = PH.derive_batch(simulation_inputs, n, species=species, n_rydberg=n_rydberg, qubit_0=qubit_0,
                         qubit_1=qubit_1, hilbert_space_dim=hilbert_space_dim,
                         tweezer_power=tweezer_power, tweezer_waist=tweezer_waist,
@@ -349,12 +352,16 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
         states = {"ket": np.zeros((nn, 4, D), complex), "rho": np.zeros((nn, 4, D, D), complex)}
     eng = _engine(devices)
     kms = 0.0
+    t_derived = time.perf_counter()
+    engine_s = 0.0
     for evol, mask in (("ket", ket_mask), ("lindblad", ~ket_mask)):
         idx = np.nonzero(mask)[0]
         if idx.size == 0:
             continue
+        t0 = time.perf_counter()
         r = eng.run(E.pack_params(b, idx), key, evol, shape=shape,
                     method=method if dim == 3 else "chebyshev", dim=dim)
+        engine_s += time.perf_counter() - t0
         kms += r.kernel_ms
         status[idx] |= r.status
         P = r.populations()
@@ -387,9 +394,12 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     out_states = None
     if return_states:
         out_states = states
+    t_end = time.perf_counter()
+    timings = {"derive_ms": (t_derived - t_start) * 1e3, "engine_ms": engine_s * 1e3,
+               "epilogue_ms": (t_end - t_derived - engine_s) * 1e3, "total_ms": (t_end - t_start) * 1e3}
     return BatchResult(batch=b, avg_fidelity=avg, fidelities=fids, populations=pops,
                        controlled_phase=cp, cz_phase_fidelity=pen, status=status,
-                       is_mixed=~ket_mask, states=out_states, kernel_ms=kms)
+                       is_mixed=~ket_mask, states=out_states, kernel_ms=kms, timings=timings)
 
 
 def noise_breakdown_row(b: PH.DerivedBatch, i: int, n_collapse_ops: Optional[int] = None) -> Dict[str, Any]:

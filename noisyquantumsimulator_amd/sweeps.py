@@ -46,6 +46,16 @@ def omega_delta_grid(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.
     480 nm leg power (Omega ∝ sqrt(P2)); Delta/Omega = linspace(0.30, 0.45);
     Omega*tau = 4.29268; V = C6/R^6 = 2pi x 1233.83 MHz; every noise rate from the
     reference formulas per point."""
+    si, n, kw = omega_delta_call(n_omega, n_delta, omega_mhz, delta_over_omega, omega_tau, include_noise,
+                                 delta_slice)
+    return PH.derive_batch(si, n=n, **kw)
+
+
+def omega_delta_call(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.0),
+                     delta_over_omega=(0.30, 0.45), omega_tau: float = 4.29268,
+                     include_noise: bool = True, delta_slice: Optional[slice] = None):
+    """The C2 grid as (simulation_inputs, n, keyword arguments) of derive_batch /
+    simulate_CZ_gate_batch (the end-to-end form of omega_delta_grid)."""
     warnings.simplefilter("ignore")
     exc = medium_excitation()
     ref = PH.derive_batch(CF.LPSimulationInputs(excitation=exc), **_apparatus_kwargs(),
@@ -58,8 +68,8 @@ def omega_delta_grid(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.
     OM, DOM = np.meshgrid(om, dom, indexing="ij")
     p2 = MEDIUM["laser_2_power"] * (OM.ravel() / om0) ** 2
     si = CF.LPSimulationInputs(excitation=exc, omega_tau=omega_tau)
-    return PH.derive_batch(si, n=p2.size, **_apparatus_kwargs(), include_noise=include_noise,
-                           overrides=dict(laser_2_power=p2, delta_over_omega=DOM.ravel()))
+    return si, p2.size, dict(**_apparatus_kwargs(), include_noise=include_noise,
+                             overrides=dict(laser_2_power=p2, delta_over_omega=DOM.ravel()))
 
 
 def pareto_tgate_grid(n_omega: int = 1000, n_tau: int = 100, include_noise: bool = True,

@@ -128,3 +128,25 @@ def test_stable_point_not_flagged_and_matches_oracle():
     cp, pen = SIM._cp_penalty(ph)
     assert flags[0] & N.STATUS_GAUGE_UNSTABLE == 0
     assert pen[0] == pytest.approx(info["cz_phase_fidelity"], abs=1e-10)
+
+
+def test_private_lapack_pool_is_bit_identical():
+    """Threads run on private dlmopen copies of scipy's OpenBLAS (ryd_lapack_pool); every
+    phase and gauge flag equals the one-thread run on scipy's own zheevr, and a sample
+    equals scipy.linalg.eigh bit for bit."""
+    rng = np.random.default_rng(3)
+    blocks = [S for _, S in _noisy_fixture_states()]
+    n = 600
+    st = np.zeros((25, 4 * n))
+    for i in range(n):
+        S = blocks[i % len(blocks)]
+        st[:, 4 * i:4 * i + 4] = S * (1.0 + 1e-6 * rng.standard_normal(S.shape)) * (np.abs(S) > 1e-15)
+    size = N.scipy_lapack_pool(4)
+    assert size >= 2, "no private LAPACK copy could be loaded"
+    ph1, f1 = E.mixed_phase(st, n, 3, gauge_check=True, n_threads=1)
+    ph4, f4 = E.mixed_phase(st, n, 3, gauge_check=True, n_threads=4)
+    assert np.array_equal(ph1, ph4) and np.array_equal(f1, f4)
+    for i in range(0, n, 37):
+        for x in range(4):
+            w, U = sla.eigh(expand_like_host(st[:, 4 * i + x]))
+            assert np.angle(U[IDX[x], int(np.argmax(w))]) == ph4[i, x]
