@@ -55,14 +55,17 @@ N_OMEGA, N_DELTA = 100, 100
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
-def _measured_traffic(workload: str, method: str, n: int):
+def _measured_traffic(workload: str, method: str, n: int, kernel: str):
+    """The committed PMC HBM-traffic row (tools/pmc_traffic.py) for this workload, size
+    and dominant kernel, or None."""
     try:
         with open(TRAFFIC_FILE) as f:
             rows = json.load(f)
     except (OSError, ValueError):
         return None
     for r in rows:
-        if r.get("workload") == workload and r.get("method") == method and r.get("n") == n:
+        if (r.get("workload") == workload and r.get("method") == method and r.get("n") == n
+                and r.get("kernel") == kernel):
             return r
     return None
 
@@ -169,14 +172,19 @@ def run_c5(args, ws, rank, local, pg):
     _barrier(pg)
     db.synchronize()
     t0 = time.perf_counter()
+    db.mark(0)
     for _ in range(args.steps):
         db.launch()
+    db.mark(1)
     db.synchronize()
     _barrier(pg)
     dt = time.perf_counter() - t0
     dt_max = _max_over_ranks(pg, dt)
-    kms = [db.launch(timed=True) for _ in range(max(3, min(args.steps, 10)))]
-    k_ms = float(np.mean(kms))
+    # the dominant kernel's average launch duration: HIP events on its stream over the
+    # timed region (back-to-back launches; the only work on that stream)
+    k_ms = db.mark_elapsed() / args.steps
+    # one launch at a time, events around each (includes event/sync overhead)
+    k_iso = float(np.mean([db.launch(timed=True) for _ in range(max(3, min(args.steps, 10)))]))
     res = db.fetch()
     assert np.all(res.status == 0), "engine reported per-point failures"
     it_use = float(res.col("ITER_USEFUL").sum())
@@ -185,7 +193,7 @@ def run_c5(args, ws, rank, local, pg):
              + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     achieved_gbs = C5_BYTES_PER_POINT * n / (k_ms * 1e-3) / 1e9
-    tr = _measured_traffic("c5", "mcwf", n) if args.n_traj == 256 else None
+    tr = _measured_traffic("c5", "mcwf", n, "traj3_kernel") if args.n_traj == 256 else None
     traffic = tr["bytes_per_launch"] if tr else None
     total = SW.C5_POINTS * args.steps
     out = {
@@ -200,7 +208,7 @@ def run_c5(args, ws, rank, local, pg):
                    "trajectories_per_s": total * args.n_traj / dt_max,
                    "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS"},
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel_ms": k_ms,
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": "traj3_kernel", "kernel_ms": k_ms, "kernel_ms_isolated": k_iso,
                      "flops_per_launch": flops, "exec_over_useful": it_exec / max(it_use, 1.0),
                      "mean_jumps": float(res.col("MEAN_JUMPS").mean())},
         "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -266,16 +274,20 @@ def main():
     _barrier(pg)
     db.synchronize()
     t0 = time.perf_counter()
+    db.mark(0)
     for _ in range(args.steps):
         db.launch()
+    db.mark(1)
     db.synchronize()
     _barrier(pg)
     dt = time.perf_counter() - t0
     dt_max = _max_over_ranks(pg, dt)
+    # the dominant kernel's average launch duration: HIP events on its stream over the
+    # timed region (back-to-back launches; the only work on that stream)
+    k_ms = db.mark_elapsed() / args.steps
 
-    # kernel device time with HIP events on the launch stream (roofline)
-    kms = [db.launch(timed=True) for _ in range(max(3, min(args.steps, 10)))]
-    k_ms = float(np.mean(kms))
+    # one launch at a time, events around each (includes event/sync overhead)
+    k_iso = float(np.mean([db.launch(timed=True) for _ in range(max(3, min(args.steps, 10)))]))
     res = db.fetch()
     assert np.all(res.status == 0), "engine reported per-point failures"
     # algorithmic bytes per launch: 15 param columns read, 25x4 state + 19 summary doubles
@@ -296,7 +308,13 @@ def main():
             upd = FLOP_PER_STATE_UPDATE_SYM if E.symmetric_atoms(params) else FLOP_PER_STATE_UPDATE
         flops += n_seg * n * upd                         # R <- U R once per reference segment
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
-    tr = _measured_traffic(args.workload, args.method, n)
+    if sym16:
+        dom_kernel = "lindblad_sym16_kernel"
+    elif args.workload == "c3" and prop_kernel:
+        dom_kernel = "jp_frame_kernel"
+    else:
+        dom_kernel = "lindblad_prop_kernel" if prop_kernel else "lindblad_cheb_kernel"
+    tr = _measured_traffic(args.workload, args.method, n, dom_kernel)
     traffic = tr["bytes_per_launch"] if tr else None
 
     # the host-buffer form of the boundary (ryd_run_batch: params H2D, kernel, state +
@@ -340,7 +358,8 @@ def main():
         # kept beside it: the kernel moves ~1 kB per point against ~1 MFLOP.
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                     "traffic": traffic, "kernel_ms": k_ms, "flops_per_launch": flops,
+                     "traffic": traffic, "kernel": dom_kernel, "kernel_ms": k_ms, "kernel_ms_isolated": k_iso,
+                     "flops_per_launch": flops,
                      "exec_over_useful": res.matvec_exec / max(res.matvec_useful, 1)},
         "host_path": host_path,
         "end_to_end": out_e2e if args.workload == "c2" and ws == 1 else None,

@@ -351,6 +351,12 @@ int ryd_lapack_pool(void* ref_zheevr, const char* path, const char* zheevr_symbo
 #define RYD_TL_SLOT 6
 int ryd_last_timeline(ryd_handle* h, double* out, int64_t cap);
 
+/* Region timing on a slot's stream: ryd_mark(h, slot, 0) ... launches ...
+ * ryd_mark(h, slot, 1); ryd_mark_elapsed waits for mark 1 and returns the device time
+ * between the two (HIP events on the stream the *_device calls use by default). */
+int ryd_mark(ryd_handle* h, int slot, int mark);
+int ryd_mark_elapsed(ryd_handle* h, int slot, float* ms);
+
 /* Minimal device-memory plumbing so callers need no other GPU runtime. */
 int ryd_malloc(ryd_handle* h, int slot, size_t bytes, void** d_ptr);
 int ryd_free(ryd_handle* h, int slot, void* d_ptr);

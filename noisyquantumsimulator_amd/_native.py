@@ -57,7 +57,7 @@ EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary
             "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",
             "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
             "ryd_run_trajectories", "ryd_run_trajectories_device",
-            "ryd_mixed_phase", "ryd_lapack_pool", "ryd_last_timeline",
+            "ryd_mixed_phase", "ryd_lapack_pool", "ryd_last_timeline", "ryd_mark", "ryd_mark_elapsed",
             "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize")
 
 
@@ -127,6 +127,8 @@ def load() -> ctypes.CDLL:
         lib.ryd_mixed_phase.argtypes = [vp, ctypes.c_int, dp, i64, i64, ctypes.c_int, ctypes.c_double,
                                         ctypes.c_double, ctypes.c_int, dp, i64, ctypes.POINTER(ctypes.c_uint32)]
         lib.ryd_last_timeline.argtypes = [vp, dp, i64]
+        lib.ryd_mark.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        lib.ryd_mark_elapsed.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
         lib.ryd_lapack_pool.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_int)]
         lib.ryd_malloc.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)]

@@ -53,6 +53,7 @@ struct ryd_slot_work {
   size_t hcap = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool ev_ok = false;
+  hipEvent_t mark[2] = {nullptr, nullptr};   // ryd_mark / ryd_mark_elapsed
 };
 
 // one stream per device slot; defined at global scope (the header's opaque type)
@@ -2403,6 +2404,8 @@ void release_slot_work(ryd_slot_work& w) {
   if (w.hbuf) (void)hipHostFree(w.hbuf);
   for (int j = 0; j < 4; ++j)
     if (w.ev[j]) (void)hipEventDestroy(w.ev[j]);
+  for (int j = 0; j < 2; ++j)
+    if (w.mark[j]) (void)hipEventDestroy(w.mark[j]);
   w = ryd_slot_work();
 }
 
@@ -2677,6 +2680,29 @@ int ryd_last_timeline(ryd_handle* h, double* out, int64_t cap) {
   if (h->timeline.empty()) return fail(RYD_ERR_INVALID, "no host-buffer call on this handle yet");
   if (cap < (int64_t)h->timeline.size()) return fail(RYD_ERR_INVALID, "timeline buffer too small");
   memcpy(out, h->timeline.data(), sizeof(double) * h->timeline.size());
+  return RYD_OK;
+}
+
+int ryd_mark(ryd_handle* h, int slot, int mark) {
+  if (!h || slot < 0 || slot >= (int)h->dev.size() || mark < 0 || mark > 1) return fail(RYD_ERR_INVALID, "bad args");
+  std::lock_guard<std::mutex> lock(h->mu);
+  if ((int)h->work.size() < (int)h->dev.size()) h->work.resize(h->dev.size());
+  ryd_slot_work& w = h->work[slot];
+  HIPCHK(hipSetDevice(h->dev[slot]));
+  if (!w.mark[mark]) HIPCHK(hipEventCreate(&w.mark[mark]));
+  HIPCHK(hipEventRecord(w.mark[mark], h->stream[slot]));
+  return RYD_OK;
+}
+
+int ryd_mark_elapsed(ryd_handle* h, int slot, float* ms) {
+  if (!h || !ms || slot < 0 || slot >= (int)h->dev.size()) return fail(RYD_ERR_INVALID, "bad args");
+  std::lock_guard<std::mutex> lock(h->mu);
+  if ((int)h->work.size() <= slot || !h->work[slot].mark[0] || !h->work[slot].mark[1])
+    return fail(RYD_ERR_INVALID, "ryd_mark 0 and 1 not recorded on this slot");
+  ryd_slot_work& w = h->work[slot];
+  HIPCHK(hipSetDevice(h->dev[slot]));
+  HIPCHK(hipEventSynchronize(w.mark[1]));
+  HIPCHK(hipEventElapsedTime(ms, w.mark[0], w.mark[1]));
   return RYD_OK;
 }
 

@@ -331,6 +331,16 @@ class DeviceBatch:
             ctypes.byref(ms) if timed else None))
         return float(ms.value)
 
+    def mark(self, which: int):
+        """Record HIP event `which` (0 = region start, 1 = region end) on the launch stream."""
+        N.check(self.eng.lib.ryd_mark(self.eng.handle, self.slot, which))
+
+    def mark_elapsed(self) -> float:
+        """Device ms between marks 0 and 1 (waits for mark 1)."""
+        ms = ctypes.c_float(0.0)
+        N.check(self.eng.lib.ryd_mark_elapsed(self.eng.handle, self.slot, ctypes.byref(ms)))
+        return float(ms.value)
+
     def synchronize(self):
         N.check(self.eng.lib.ryd_synchronize(self.eng.handle))
 

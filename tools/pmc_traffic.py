@@ -57,7 +57,7 @@ def main():
     if os.path.exists(a.out):
         with open(a.out) as f:
             rows = [r for r in json.load(f)
-                    if (r["workload"], r["method"], r["n"]) != (a.workload, a.method, a.n)]
+                    if (r["workload"], r["method"], r["n"], r["kernel"]) != (a.workload, a.method, a.n, a.kernel)]
     rows.append(row)
     with open(a.out, "w") as f:
         json.dump(rows, f, indent=1)
