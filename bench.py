@@ -165,6 +165,7 @@ def run_c5(args, ws, rank, local, pg):
     n = batch.n
     eng = E.Engine(devices=[local])
     db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=args.n_traj,
+                                  ladder_levels=args.ladder if args.ladder > 0 else TR.DEFAULT_LADDER,
                                   seed=20260215, point_offset=off)
     for _ in range(args.warmup):
         db.launch()
@@ -206,7 +207,8 @@ def run_c5(args, ws, rank, local, pg):
                                 "per point (Philox4x32-10), |+++> input, medium-apparatus rates"),
                    "points_per_gpu": n, "global_points": SW.C5_POINTS, "trajectories_per_point": args.n_traj,
                    "trajectories_per_s": total * args.n_traj / dt_max,
-                   "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS"},
+                   "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS",
+                   "ladder_levels": db.desc.ladder_levels},
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": "traj3_kernel", "kernel_ms": k_ms, "kernel_ms_isolated": k_iso,
                      "flops_per_launch": flops, "exec_over_useful": it_exec / max(it_use, 1.0),
@@ -237,6 +239,7 @@ def main():
                     choices=["chebyshev", "cheb_squaring", "cheb_vector"])
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--n-traj", type=int, default=256, help="C5 trajectories per point")
+    ap.add_argument("--ladder", type=int, default=0, help="C5 ladder levels (0: trajectories.DEFAULT_LADDER)")
     args = ap.parse_args()
 
     ws, rank, local, pg = _dist()

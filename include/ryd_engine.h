@@ -194,7 +194,7 @@ typedef struct ryd_traj_desc {
   int32_t shape;           /* RYD_SHAPE_* (LP_SHAPED) */
   int32_t n_steps;         /* as ryd_batch_desc */
   int32_t n_traj;          /* trajectories per point: a multiple of 64 */
-  int32_t ladder_levels;   /* 1 .. RYD_T_LADDER_MAX (24 recommended) */
+  int32_t ladder_levels;   /* 1 .. RYD_T_LADDER_MAX (16 recommended) */
   uint64_t seed;
   double psi0[2 * RYD_T_DIM];  /* normalised initial ket, (re, im) interleaved */
 } ryd_traj_desc;
