@@ -37,6 +37,10 @@ FLOP_PER_MATVEC = 2 * (75 + 75 + 12 + 25)
 # identical atoms: the symmetric column on its 15-entry triangle (apply_Lsym): every
 # output (i <= j) costs row i + row j of M (1, 3, 3, 4, 4 ops), V 6, Clenshaw 15
 FLOP_PER_MATVEC_SYM = 2 * (6 * (1 + 3 + 3 + 4 + 4) + 6 + 15)
+# the 16-lane DPP-row kernel builds phase-0 propagators only (real Rabi frequency, hy = 0):
+# rows 0-4 of M cost 1, 2, 2, 2 FMAs and 3 FMAs + 1 subtraction (2, 4, 4, 4, 7 flops) per
+# output, V 6 FMAs, the unit start vector's Clenshaw term 1 add on the lane's own coordinate
+FLOP_PER_MATVEC_SYM16 = 6 * (2 + 4 + 4 + 4 + 7) + 2 * 6 + 1
 FLOP_PER_SQUARING = 2 * 25 ** 3          # one 25x25 real matrix product
 # identical atoms: only the block-triangular symmetric block [[B, C], [0, D]] (5 + 10):
 # B^2 (125) + BC + CD (250 + 500) + D^2 (1000) FMAs
@@ -304,6 +308,8 @@ def main():
     flops = res.matvec_useful * mv_flops + nsq * sq_flops
     sym16 = (args.method == "chebyshev" and E.symmetric_atoms(params)
              and os.environ.get("RYD_SYM16", "1") != "0")
+    if sym16:
+        flops = res.matvec_useful * FLOP_PER_MATVEC_SYM16 + nsq * sq_flops
     if prop_kernel:
         if sym16:
             upd = FLOP_PER_STATE_UPDATE_SYM16
