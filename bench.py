@@ -309,12 +309,14 @@ def main():
     sym16 = (args.method == "chebyshev" and E.symmetric_atoms(params)
              and os.environ.get("RYD_SYM16", "1") != "0")
     if sym16:
-        flops = res.matvec_useful * FLOP_PER_MATVEC_SYM16 + nsq * sq_flops
-    if prop_kernel:
-        if sym16:
-            upd = FLOP_PER_STATE_UPDATE_SYM16
-        else:
-            upd = FLOP_PER_STATE_UPDATE_SYM if E.symmetric_atoms(params) else FLOP_PER_STATE_UPDATE
+        # LP square leaves the last min(s, K) squaring levels to the states: per point
+        # s - min(s, K) squarings and 2^min(s, K) state updates per segment (one build)
+        sd = res.col("NSQUARE")
+        rep = np.minimum(sd, eng.lib.ryd_lp_unsquared()) if protocol == "lp_square" else np.zeros(n)
+        flops = (res.matvec_useful * FLOP_PER_MATVEC_SYM16 + float((sd - rep).sum()) * sq_flops
+                 + n_seg * float(np.exp2(rep).sum()) * FLOP_PER_STATE_UPDATE_SYM16)
+    elif prop_kernel:
+        upd = FLOP_PER_STATE_UPDATE_SYM if E.symmetric_atoms(params) else FLOP_PER_STATE_UPDATE
         flops += n_seg * n * upd                         # R <- U R once per reference segment
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     if sym16:

@@ -127,7 +127,11 @@ extern "C" {
 #define RYD_S_NMV_USEFUL 16  /* generator applications needed, whole point (flop accounting) */
 #define RYD_S_NMV_EXEC   17  /* generator applications executed, whole point (wave-uniform)  */
 #define RYD_S_TRACE11    18  /* Tr rho_11 (Lindblad sanity), ket: |psi_11|^2              */
-#define RYD_S_NSQUARE    19  /* 25x25 squarings performed (squaring method)               */
+#define RYD_S_NSQUARE    19  /* scaling-and-squaring depth s: the propagator is exp(L dt / 2^s)^(2^s),
+                                * summed over the point's builds.  Every kernel performs s matrix
+                                * squarings, except the identical-atom LP-square path, which performs
+                                * s - min(s, ryd_lp_unsquared()) and applies the remaining
+                                * 2^min(s, ryd_lp_unsquared()) factor to the states segment by segment */
 #define RYD_NSUMMARY     20
 
 /* ---- process-map coherences (ryd_run_coherences), rows of out_coh ----------
@@ -251,6 +255,8 @@ const char* ryd_last_error(void);
 int         ryd_param_count(void);
 int         ryd_summary_width(void);
 int         ryd_state_width(int evolution, int dim);
+/* squaring levels the identical-atom LP-square kernel leaves unsquared (see RYD_S_NSQUARE) */
+int         ryd_lp_unsquared(void);
 int         ryd_device_count(int* count);
 
 int ryd_create(const int* device_ids, int n_devices, ryd_handle** out);

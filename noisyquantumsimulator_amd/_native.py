@@ -53,7 +53,7 @@ T_NSUMMARY = 10
 # ryd_last_timeline layout
 TL_HEAD, TL_SLOT = 4, 6
 
-EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary_width",
+EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary_width", "ryd_lp_unsquared",
             "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",
             "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
             "ryd_run_trajectories", "ryd_run_trajectories_device",
@@ -107,6 +107,7 @@ def load() -> ctypes.CDLL:
         lib.ryd_last_error.restype = ctypes.c_char_p
         lib.ryd_param_count.restype = ctypes.c_int
         lib.ryd_summary_width.restype = ctypes.c_int
+        lib.ryd_lp_unsquared.restype = ctypes.c_int
         lib.ryd_state_width.argtypes = [ctypes.c_int, ctypes.c_int]
         lib.ryd_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         lib.ryd_create.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(vp)]

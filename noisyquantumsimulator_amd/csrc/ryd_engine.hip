@@ -1596,6 +1596,9 @@ __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
 #ifndef RYD_S16_WAVES
 #define RYD_S16_WAVES 3                      // waves per SIMD the sym16 register budget targets
 #endif
+#ifndef RYD_LP_UNSQUARED
+#define RYD_LP_UNSQUARED 2                   // LP square, identical atoms: squaring levels left to the states
+#endif
 #include "ryd_sym16.inc"
 
 // ---------------------------------------------------------------------------
@@ -2586,6 +2589,7 @@ int ryd_abi_version(void) { return RYD_ABI_VERSION; }
 const char* ryd_last_error(void) { return g_err.c_str(); }
 int ryd_param_count(void) { return RYD_NPARAM; }
 int ryd_summary_width(void) { return RYD_NSUMMARY; }
+int ryd_lp_unsquared(void) { return RYD_LP_UNSQUARED; }
 int ryd_state_width(int evolution, int dim) {
   if (dim != 3 && dim != 4) return -1;
   if (evolution == RYD_EVOL_LINDBLAD) return dim == 3 ? 25 : 36;

