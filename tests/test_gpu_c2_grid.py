@@ -66,3 +66,22 @@ def test_c2_grid_populations_across_sweep():
     assert np.linalg.eigvalsh(rho).min() > -1e-11
     p11 = pops[:, 3].reshape(100, 100)
     assert np.max(np.abs(np.diff(p11, 2, axis=0))) < 0.05
+
+
+def test_dopri5_at_full_c2_stiffness():
+    """The reference-style adaptive stepper (RYD_METHOD_DOPRI5) on the bench's own
+    corners, at the real blockade (V/2pi = 1234 MHz, V tau up to 5e3 rad) and the
+    reference's mesolve tolerances (rtol 1e-8, atol 1e-10, RG/simulation.py:683-690):
+    it agrees with the exact propagator to the stepper's own error, the ZVODE-level
+    ~1e-7 of SURVEY.md section 7 hard part 1 (populations 1e-7, rho elements 1e-6), and
+    needs orders of magnitude more generator applications."""
+    warnings.simplefilter("ignore")
+    b = SW.omega_delta_grid()
+    p = E.pack_params(b)[:, np.array(CHECK)].copy()
+    eng = SIM._engine()
+    ex = eng.run(p, "lp_square", "lindblad")
+    rk = eng.run(p, "lp_square", "lindblad", method="dopri5", rtol=1e-8, atol=1e-10, max_steps=10 ** 7)
+    assert np.all(rk.status == 0) and np.all(ex.status == 0)
+    np.testing.assert_allclose(rk.populations(), ex.populations(), atol=1e-7, rtol=0)
+    np.testing.assert_allclose(rk.state, ex.state, atol=1e-6, rtol=0)
+    assert rk.matvec_useful > 20 * ex.matvec_useful
