@@ -1594,7 +1594,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void jp_frame_kernel(
 }
 
 #ifndef RYD_S16_WAVES
-#define RYD_S16_WAVES 3                      // waves per SIMD the sym16 register budget targets
+#define RYD_S16_WAVES 4                      // waves per SIMD the sym16 register budget targets (LP: 128 VGPRs, no scratch)
 #endif
 #ifndef RYD_LP_UNSQUARED
 #define RYD_LP_UNSQUARED 2                   // LP square, identical atoms: squaring levels left to the states
