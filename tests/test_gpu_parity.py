@@ -309,3 +309,35 @@ def test_dopri5_reference_stepper(eng, protocol, n_steps):
     assert r.matvec_useful > 5 * ex.matvec_useful / 4      # stepper needs many more RHS calls
     capped = eng.run(p[:, :2], protocol, "lindblad", n_steps=n_steps, method="dopri5", max_steps=5)
     assert np.all(capped.status & N.STATUS_STEP_CAP)
+
+
+def test_sym16_invalid_waves_and_phase_range(eng):
+    """Identical-atom (sym16) edge cases: a whole wave of invalid points (segment 0 still
+    builds, identity rows) beside valid waves; a smooth-JP point whose laser-phase
+    argument leaves the inlined sin/cos range (|x| >= 1e15) is flagged NONFINITE alone,
+    the rest of its wave unaffected and equal to a clean run."""
+    rng = np.random.default_rng(29)
+    for protocol, ns in (("lp_square", None), ("bangbang", None)):
+        p = _random_points(rng, 12, protocol)
+        for k in ("G1", "G0", "GPHI", "GSC"):
+            p[N.P[k + "_B"]] = p[N.P[k + "_A"]]
+        assert E.symmetric_atoms(p)
+        p[N.P["OMEGA"], 4:8] = 0.0                        # the second wave: all invalid
+        r = eng.run(p, protocol, "lindblad", n_steps=ns)
+        assert np.all(r.status[4:8] & N.STATUS_BAD_INPUT)
+        ok = np.r_[0:4, 8:12]
+        assert np.all(r.status[ok] == 0)
+        clean = eng.run(p[:, ok].copy(), protocol, "lindblad", n_steps=ns)
+        np.testing.assert_array_equal(clean.state, r.state.reshape(25, 12, 4)[:, ok].reshape(25, -1))
+    p = _random_points(rng, 8, "smooth_jp")
+    for k in ("G1", "G0", "GPHI", "GSC"):
+        p[N.P[k + "_B"]] = p[N.P[k + "_A"]]
+    base = eng.run(p, "smooth_jp", "lindblad", n_steps=60)
+    assert np.all(base.status == 0)
+    p[N.P["OMEGA_MOD"], 2] = 1e25                          # phase argument ~1e19 rad
+    r = eng.run(p, "smooth_jp", "lindblad", n_steps=60)
+    assert r.status[2] & N.STATUS_NONFINITE
+    others = [i for i in range(8) if i != 2]
+    assert np.all(r.status[others] == 0)
+    st = r.state.reshape(25, 8, 4)
+    np.testing.assert_array_equal(st[:, others], base.state.reshape(25, 8, 4)[:, others])
