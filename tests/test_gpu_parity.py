@@ -247,6 +247,13 @@ def test_squaring_and_vector_methods_agree(eng, protocol, n_steps, symmetric):
     ref = _oracle_point(p, 44, protocol, n_steps=n_steps or 300)
     for k, lab in enumerate(O.LABELS):
         np.testing.assert_allclose(rs.rho()[44, k], ref[lab], atol=TOL, rtol=0)
+    if symmetric:
+        # the 16-lane DPP-row kernel (auto method for identical atoms: segment order, inlined
+        # sin/cos, angle recurrence, LDS zero words) is a third evaluation of the same map
+        r16 = eng.run(p, protocol, "lindblad", n_steps=n_steps, method="chebyshev")
+        assert np.all(r16.status == 0)
+        np.testing.assert_allclose(r16.state, rv.state, atol=1e-11, rtol=0)
+        np.testing.assert_allclose(r16.populations(), rv.populations(), atol=1e-11, rtol=0)
 
 
 def test_lp_phase_frame_fallback_for_non_unit_xi(eng):
