@@ -191,7 +191,7 @@ __device__ __forceinline__ void h_bounds(const Seg& g, double V, double d1, doub
 #pragma unroll
   for (int a1 = 0; a1 < 3; ++a1)
 #pragma unroll
-    for (int a2 = 0; a2 < 3; ++a2) {
+    for (int a2 = a1; a2 < 3; ++a2) {        // (a1, a2) and (a2, a1) give the same bounds
       const double E = e[a1] + e[a2] + ((a1 == 2 && a2 == 2) ? V : 0.0);
       const double r = w * ((a1 ? 1.0 : 0.0) + (a2 ? 1.0 : 0.0));
       emin = fmin(emin, E - r);
