@@ -19,8 +19,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _heavy_params(n_omega=100):
-    """10k smooth-JP points, 4-op model; with 3000 segments each slot's kernel runs
-    for milliseconds, long against the host pack of the next slot."""
+    """10k smooth-JP points, 4-op model; with 12000 segments each slot's kernel runs
+    for milliseconds, long against the host pack of the next slot (3000 segments gave
+    ~0.6 ms kernels by the end of round 2, about the pack time: the overlap flickered)."""
     warnings.simplefilter("ignore")
     return SW.c3_four_op_params(SW.pareto_tgate_grid(n_omega=n_omega, n_tau=100))
 
@@ -29,9 +30,9 @@ def test_two_slot_handle_overlaps_and_matches_one_slot():
     p = _heavy_params()
     one = E.Engine(devices=[0])
     two = E.Engine(devices=[0, 0])
-    r1 = one.run(p, "smooth_jp", "lindblad", n_steps=3000)
-    two.run(p, "smooth_jp", "lindblad", n_steps=3000)          # warm the workspace
-    r2 = two.run(p, "smooth_jp", "lindblad", n_steps=3000)
+    r1 = one.run(p, "smooth_jp", "lindblad", n_steps=12000)
+    two.run(p, "smooth_jp", "lindblad", n_steps=12000)          # warm the workspace
+    r2 = two.run(p, "smooth_jp", "lindblad", n_steps=12000)
     assert np.all(r1.status == 0) and np.all(r2.status == 0)
     assert np.array_equal(r1.state, r2.state)
     assert np.array_equal(r1.summary, r2.summary, equal_nan=True)   # Lindblad OV rows are NaN
