@@ -12,7 +12,8 @@ over the ranks (strong scaling: the global grid is fixed); ``--workload c5`` the
 4096-point three-atom blockade grid with 256 quantum-jump trajectories per point
 (BASELINE configs[4]), strong-scaled the same way.  These are secondary lines,
 not the metric.  With N > 1
-ranks (torch.distributed.run, one process per GPU) the global sweep is N x 10k
+ranks (one process per GPU: under torch.distributed.run, or started by this script
+itself when ``--gpus N`` is given without WORLD_SIZE in the environment) the global sweep is N x 10k
 points range-partitioned by Delta/Omega; no collective touches the data path
 (weak scaling); a gloo barrier brackets the timed region and the max time over
 ranks is reported.  Rank 0 prints one JSON line.
@@ -84,6 +85,90 @@ def _dist():
         dist.init_process_group("gloo")
         pg = dist
     return ws, rank, local, pg
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, timeout_s: float = 0.0) -> int:
+    """``--gpus N`` without a launcher around us: start N rank processes of this script
+    (one per GPU) and wait for them.  The parent makes no GPU call (it never imports the
+    engine or torch), so nothing here initialises HIP before the children start; each
+    child is a fresh interpreter with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, maps
+    LOCAL_RANK -> device LOCAL_RANK % device_count, and rank 0 prints the JSON line on the
+    inherited stdout.  If any rank fails the others are stopped (they would wait at the
+    barrier forever) and the first failing exit code is returned."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+    t0 = time.monotonic()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+        if rc != 0 or (timeout_s > 0 and time.monotonic() - t0 > timeout_s):
+            for p in live:              # our own children, by PID
+                p.terminate()
+            for p in live:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            if rc == 0:
+                rc = 124
+            break
+        time.sleep(0.05)
+    return rc
+
+
+def _rank_device(local: int) -> int:
+    """LOCAL_RANK -> HIP device: LOCAL_RANK % visible devices (ranks share a device when
+    N exceeds the devices: a functional run, not a scaling point)."""
+    from noisyquantumsimulator_amd import engine as E
+    return local % E.device_count()
+
+
+def _placement(ws: int, local: int, dev: int) -> dict:
+    from noisyquantumsimulator_amd import engine as E
+    cnt = E.device_count()
+    shared = ws > cnt
+    return {"device": dev, "visible_devices": cnt, "ranks_share_devices": shared,
+            "note": ("ranks share devices (N > visible GPUs): functional check of the N-rank path, "
+                     "not a scaling point") if shared else "one rank per GPU"}
+
+
+def run_stub(ws, rank, local, pg):
+    """GPU-free rank body for the launcher test: every rank reports its environment, rank
+    0 prints them as one JSON line after a barrier."""
+    info = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}
+    info["pid"] = os.getpid()
+    if os.environ.get("RYD_BENCH_STUB_FAIL_RANK") == str(rank):
+        sys.exit(3)          # launcher test: a failing rank must fail the job
+    ranks = [info]
+    if pg is not None:
+        ranks = [None] * ws
+        pg.all_gather_object(ranks, info)
+        _barrier(pg)
+    if rank == 0:
+        print(json.dumps({"stub": True, "n_ranks": ws, "ranks": ranks}), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
 
 
 def _barrier(pg):
@@ -167,7 +252,8 @@ def run_c5(args, ws, rank, local, pg):
     batch, off = SW.c5_rank_shard(rank, ws)
     params = E.pack_params(batch)
     n = batch.n
-    eng = E.Engine(devices=[local])
+    dev = _rank_device(local)
+    eng = E.Engine(devices=[dev])
     db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=args.n_traj,
                                   ladder_levels=args.ladder if args.ladder > 0 else TR.DEFAULT_LADDER,
                                   seed=20260215, point_offset=off)
@@ -212,7 +298,7 @@ def run_c5(args, ws, rank, local, pg):
                    "points_per_gpu": n, "global_points": SW.C5_POINTS, "trajectories_per_point": args.n_traj,
                    "trajectories_per_s": total * args.n_traj / dt_max,
                    "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS",
-                   "ladder_levels": db.desc.ladder_levels},
+                   "ladder_levels": db.desc.ladder_levels, "placement": _placement(ws, local, dev)},
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": "traj3_kernel", "kernel_ms": k_ms, "kernel_ms_isolated": k_iso,
                      "flops_per_launch": flops, "exec_over_useful": it_exec / max(it_use, 1.0),
@@ -244,9 +330,15 @@ def main():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--n-traj", type=int, default=256, help="C5 trajectories per point")
     ap.add_argument("--ladder", type=int, default=0, help="C5 ladder levels (0: trajectories.DEFAULT_LADDER)")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test: no GPU
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun around us: start the N ranks ourselves (before any GPU call)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     ws, rank, local, pg = _dist()
+    if args.stub:
+        return run_stub(ws, rank, local, pg)
     if args.workload == "c5":
         return run_c5(args, ws, rank, local, pg)
     from noisyquantumsimulator_amd import engine as E
@@ -272,7 +364,8 @@ def main():
                     "medium apparatus, full reference noise model")
     params = SW.c3_four_op_params(batch) if args.workload == "c3" else E.pack_params(batch)
     n = batch.n
-    eng = E.Engine(devices=[local])
+    dev = _rank_device(local)
+    eng = E.Engine(devices=[dev])
     db = E.DeviceBatch(eng, params, protocol, "lindblad", n_steps=n_steps, method=args.method)
 
     for _ in range(args.warmup):
@@ -360,7 +453,7 @@ def main():
         "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": workload, "points_per_gpu": n, "global_points": global_points,
-                   "parallelism": f"range-shard x{ws}",
+                   "parallelism": f"range-shard x{ws}", "placement": _placement(ws, local, dev),
                    "method": args.method + ((" (auto: 16-lane DPP-row propagator kernel, phase frame)"
                                              if sym16 else " (auto: propagator kernel, phase frame)")
                                             if args.method == "chebyshev" else "")},

@@ -208,6 +208,14 @@ def symmetric_atoms(params: np.ndarray) -> bool:
                for k in ("G1", "G0", "GPHI", "GSC", "GMJ"))
 
 
+def device_count() -> int:
+    """GPUs visible to the HIP runtime (ryd_device_count)."""
+    lib = N.load()
+    cnt = ctypes.c_int(0)
+    N.check(lib.ryd_device_count(ctypes.byref(cnt)))
+    return cnt.value
+
+
 class Engine:
     """A handle on one or more GPUs (points are range-partitioned across them)."""
 
