@@ -341,7 +341,10 @@ int ryd_mixed_phase(void* zheevr, int dim, const double* state, int64_t n, int64
  * ref_zheevr then runs one instance per worker thread (min(n_threads, pool size)
  * threads): OpenBLAS serialises concurrent callers of one instance on a process-wide
  * lock.  *n_loaded = pool size (loading stops quietly when namespaces or static TLS run
- * out); an error only if no copy could be loaded. */
+ * out); an error only if no copy could be loaded.  PROCESS-WIDE SIDE EFFECT: each copy
+ * occupies a glibc link namespace and static-TLS space for the life of the process, so
+ * copies are capped at 8 and loading is attempted once per process: later calls return
+ * the first attempt's outcome (partial or failed) and never call dlmopen again. */
 int ryd_lapack_pool(void* ref_zheevr, const char* path, const char* zheevr_symbol,
                     const char* threads_symbol, int copies, int* n_loaded);
 

@@ -171,6 +171,15 @@ def scipy_zheevr() -> int:
 
 
 _pool_size: Optional[int] = None
+LAPACK_POOL_DEFAULT = 8     # copies (the C side caps at 8: each holds a glibc link namespace)
+
+
+def lapack_pool_copies(n_threads: int) -> int:
+    """Copies the epilogue asks for: RYD_LAPACK_POOL (0 = off, N = at most N copies),
+    default min(n_threads, 8)."""
+    env = os.environ.get("RYD_LAPACK_POOL")
+    cap = LAPACK_POOL_DEFAULT if env is None or env.strip() == "" else int(env)
+    return max(0, min(n_threads, cap))
 
 
 def scipy_lapack_pool(copies: int) -> int:
@@ -178,9 +187,14 @@ def scipy_lapack_pool(copies: int) -> int:
     OpenBLAS serialises concurrent zheevr callers on a process-wide lock, each copy in
     its own link namespace has its own.  Copies are admitted only if bit-identical to
     scipy_zheevr() on test matrices.  Returns the pool size (0: none could be loaded --
-    the epilogue then runs on scipy's zheevr itself, correct but serialised)."""
+    the epilogue then runs on scipy's zheevr itself, correct but serialised).
+
+    Process-wide side effect: every copy occupies a glibc link namespace (about 16 per
+    process) and static-TLS space for the life of the process.  The first call's outcome
+    -- full, partial or failed -- is cached here and in the library: later calls never
+    load again ("Host epilogue")."""
     global _pool_size
-    if _pool_size is not None and _pool_size >= copies:
+    if _pool_size is not None:
         return _pool_size
     import glob
     import scipy

@@ -72,8 +72,9 @@ def mixed_phase(state: np.ndarray, n: int, dim: int = 3, gauge_check: bool = Tru
     lib = N.load()
     if n_threads <= 0:          # the GPU box's CPU share is 16 cores per GPU (os.cpu_count() shows more)
         n_threads = int(os.environ.get("RYD_HOST_THREADS", min(16, os.cpu_count() or 1)))
-    if n_threads > 1 and n >= 64 and os.environ.get("RYD_LAPACK_POOL", "1") != "0":
-        N.scipy_lapack_pool(n_threads)
+    pool = N.lapack_pool_copies(n_threads)
+    if n_threads > 1 and n >= 64 and pool > 1:
+        N.scipy_lapack_pool(pool)
     st = np.ascontiguousarray(state, dtype=np.float64)
     out = np.zeros((N.MP_WIDTH, max(n, 1)), dtype=np.float64)
     flags = np.zeros(max(n, 1), dtype=np.uint32)

@@ -126,6 +126,24 @@ def process_fidelity(S: np.ndarray, u: np.ndarray) -> np.ndarray:
     return np.real(np.einsum("nk,nk->n", diag, np.einsum("nkk->nk", S))) / 16
 
 
+def ket_maps(psi: np.ndarray, dim: int = 3) -> np.ndarray:
+    """S (n, 16, 16) of a unitary (noise-free) evolution from the output kets psi[n, 4, D]
+    of the 4 basis inputs: <c|E(|a><b|)|d> = psi_a[c] conj(psi_b[d]) on the qubit block."""
+    q = np.array([0, 1, dim, dim + 1])                              # |00>, |01>, |10>, |11> in D
+    P = psi[:, :, q]                                                # [n, a, c]
+    return np.einsum("nac,nbd->ncdab", P, np.conj(P)).reshape(psi.shape[0], 16, 16)
+
+
+def gate_fidelity(S: np.ndarray):
+    """(process fidelity, average gate fidelity) to CZ up to the fitted local Z phases:
+    a function of the map alone, so unlike the reference's eigenvector-phase penalty it
+    does not depend on the eigensolver's gauge."""
+    al, be = cz_phase_fit(S)
+    fpro = process_fidelity(S, ideal_cz(al, be))
+    surv = np.real(S[:, ::5, ::5].sum(axis=(1, 2))) / 4
+    return fpro, (4 * fpro + surv) / 5
+
+
 @dataclass
 class ProcessMaps:
     S: np.ndarray                 # (n, 16, 16) qubit-block map on matrix units

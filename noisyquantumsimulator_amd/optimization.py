@@ -32,7 +32,7 @@ from scipy.optimize import differential_evolution
 
 from .configurations import (JPSimulationInputs, LaserParameters, LPSimulationInputs,
                              NoiseSourceConfig, TwoPhotonExcitationConfig)
-from .optimize_cz_gate import default_batch_evaluator
+from .optimize_cz_gate import COST_KINDS, default_batch_evaluator
 
 
 @dataclass
@@ -185,11 +185,17 @@ def optimize_CZ_parameters(
         maxiter: int = 100, tol: float = 1e-5, seed: Optional[int] = 42, polish: bool = True, workers: int = 1,
         popsize: int = 15, fixed_params: Optional[Dict[str, float]] = None,
         callback: Optional[Callable[[int, float, Dict], None]] = None, verbose: bool = True,
-        vectorized: bool = True, evaluator: Optional[Callable] = None) -> HardwareOptimizationResult:
+        vectorized: bool = True, evaluator: Optional[Callable] = None,
+        cost: str = "reference") -> HardwareOptimizationResult:
     """Find hardware parameters reaching a target fidelity and gate time
     (RG/optimization.py:280-739).  Objective per candidate:
     w_F (1 - F/F_t)^2 + w_t ((t - t_t)/t_t)^2 + c * penalties (V/Omega < 10,
-    spacing_factor*tweezer_waist < 2 tweezer_waist, T < 50 nK); failures cost 1e6."""
+    spacing_factor*tweezer_waist < 2 tweezer_waist, T < 50 nK); failures cost 1e6.
+    ``cost="process_fidelity"``: F is the gauge-invariant average gate fidelity to CZ
+    (optimize_cz_gate.compute_cost_batch) instead of the reference's avg F."""
+    if cost not in COST_KINDS:
+        raise ValueError(f"Unknown cost {cost!r}: use one of {COST_KINDS}")
+    ev_kw = {"process_fidelity": True} if cost == "process_fidelity" else {}
     fixed_params = dict(fixed_params or {})
     is_lp = _is_lp(protocol)
     is_jp = protocol.lower() in ("jandura_pupillo", "jp", "smooth_jp", "single_pulse", "time_optimal")
@@ -244,16 +250,17 @@ def optimize_CZ_parameters(
                    spacing_factor=g("spacing_factor"), tweezer_power=g("tweezer_power"),
                    tweezer_waist=g("tweezer_waist"), background_loss_rate_hz=background_loss_rate_hz)
         from .optimize_cz_gate import _evaluate_rows
-        m, ok = _evaluate_rows(evaluator, si, over, S, include_noise, app)
-        F, t_ns, vo = m["avg_fidelity"], m["gate_time_us"] * 1e3, m["V_over_Omega"]
+        m, ok = _evaluate_rows(evaluator, si, over, S, include_noise, app, **ev_kw)
+        F = m["avg_gate_fidelity"] if cost == "process_fidelity" else m["avg_fidelity"]
+        t_ns, vo = m["gate_time_us"] * 1e3, m["V_over_Omega"]
         sf, w, T = g("spacing_factor"), g("tweezer_waist"), g("temperature")
         pen = (np.where(vo < 10, (10 - vo) ** 2, 0.0)
                + np.where(sf * w < 2 * w, ((2 * w - sf * w) / w) ** 2, 0.0)
                + np.where(T < 0.05e-6, ((0.05e-6 - T) / 1e-6) ** 2, 0.0))
-        cost = (weight_fidelity * (1 - F / target_fidelity) ** 2
+        obj = (weight_fidelity * (1 - F / target_fidelity) ** 2
                 + weight_time * ((t_ns - target_gate_time_ns) / target_gate_time_ns) ** 2
                 + constraint_penalty * pen)
-        cost = np.where(ok & np.isfinite(cost), cost, 1e6)
+        obj = np.where(ok & np.isfinite(obj), obj, 1e6)
         for j in range(S):                     # sequential bookkeeping, as the scalar objective
             state["n"] += 1
             if not ok[j]:
@@ -261,18 +268,18 @@ def optimize_CZ_parameters(
             params = {k: float(v[j]) for k, v in P.items() if k != "laser_linewidth"}
             if "n_rydberg" in params:
                 params["n_rydberg"] = int(params["n_rydberg"])
-            if cost[j] < state["best"]:
-                state["best"] = float(cost[j])
+            if obj[j] < state["best"]:
+                state["best"] = float(obj[j])
                 bp = dict(params)
                 bp.update(laser_linewidth=float(lw[j]), _fidelity=float(F[j]), _gate_time_ns=float(t_ns[j]),
                           _V_over_Omega=float(vo[j]), _noise=_breakdown(m, j))
                 state["best_params"] = bp
             if callback is not None:
-                callback(state["n"], float(cost[j]), params)
+                callback(state["n"], float(obj[j]), params)
             if verbose and state["n"] % 20 == 0:
                 print(f"  [Eval {state['n']:4d}] F={F[j]:.4f}, t={t_ns[j]:.1f}ns, V/Omega={vo[j]:.1f}, "
-                      f"cost={cost[j]:.2e}")
-        return cost
+                      f"cost={obj[j]:.2e}")
+        return obj
 
     if verbose:
         print(f"CZ hardware optimisation: {protocol}, target F={target_fidelity:.4f}, "
@@ -331,14 +338,21 @@ def explore_parameter_space(
         bounds_temperature=(1e-6, 15e-6), bounds_spacing_factor=(2.0, 5.0), bounds_n_rydberg=(50, 90),
         bounds_tweezer_power=(10e-3, 100e-3), bounds_tweezer_waist=(0.5e-6, 2.0e-6),
         bounds_laser_linewidth=(100.0, 10e3), bounds_delta_over_omega=(0.32, 0.42),
-        bounds_omega_tau=(3.9, 4.8), evaluator: Optional[Callable] = None) -> ExplorationResult:
+        bounds_omega_tau=(3.9, 4.8), evaluator: Optional[Callable] = None,
+        cost: str = "reference") -> ExplorationResult:
     """Every DE evaluation recorded, Pareto front post hoc (RG/optimization.py:746-980).
     One engine pass per DE generation (the reference's DE already uses deferred
-    updating, so the candidate sequence is the reference's)."""
+    updating, so the candidate sequence is the reference's).  ``cost="process_fidelity"``
+    records and minimises the gauge-invariant average gate fidelity instead of the
+    reference's avg F; ``optimizer_settings["gauge_flagged"]`` counts the evaluated points
+    whose reference penalty was gauge-flagged."""
+    if cost not in COST_KINDS:
+        raise ValueError(f"Unknown cost {cost!r}: use one of {COST_KINDS}")
+    ev_kw = {"process_fidelity": True} if cost == "process_fidelity" else {}
     seeds = seeds if seeds is not None else [42 + 111 * i for i in range(n_runs)]
     result = ExplorationResult(protocol=protocol, species=species,
                                optimizer_settings=dict(n_runs=n_runs, maxiter=maxiter, popsize=popsize,
-                                                       seeds=seeds))
+                                                       seeds=seeds, cost=cost, gauge_flagged=0))
     t0 = time.time()
     is_lp = _is_lp(protocol)
     names = ["rydberg_power_2", "rydberg_power_1", "temperature", "spacing_factor", "n_rydberg",
@@ -371,8 +385,11 @@ def explore_parameter_space(
         app = dict(species=species, n_rydberg=np.round(P["n_rydberg"]), temperature=P["temperature"],
                    spacing_factor=P["spacing_factor"], tweezer_power=P["tweezer_power"],
                    tweezer_waist=P["tweezer_waist"])
-        m, ok = _evaluate_rows(evaluator, si, over, S, True, app)
-        F, t_ns = m["avg_fidelity"], m["gate_time_us"] * 1e3
+        m, ok = _evaluate_rows(evaluator, si, over, S, True, app, **ev_kw)
+        F = m["avg_gate_fidelity"] if cost == "process_fidelity" else m["avg_fidelity"]
+        t_ns = m["gate_time_us"] * 1e3
+        if "gauge_unstable" in m:
+            result.optimizer_settings["gauge_flagged"] += int((np.asarray(m["gauge_unstable"])[ok] > 0).sum())
         out = np.where(ok, (1 - F) + 0.001 * (t_ns / 1000), 1.0)
         for j in range(S):
             if not ok[j]:

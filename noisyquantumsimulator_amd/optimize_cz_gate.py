@@ -164,28 +164,53 @@ class SimulationCache:
 _global_cache = SimulationCache(precision=4)
 
 
-def compute_cost(metrics: Dict[str, float], gate_time_us: float = 0.0, time_weight: float = 0.01) -> float:
+COST_KINDS = ("reference", "process_fidelity")
+# probes of the gauge check in the optimiser and sweep paths (the full 16-probe
+# check doubles the epilogue); a flag set by any probe is still a proof, an unset one says
+# less
+OPT_GAUGE_COPIES = 4
+
+
+def compute_cost(metrics: Dict[str, float], gate_time_us: float = 0.0, time_weight: float = 0.01,
+                 cost: str = "reference") -> float:
     """Percentage-infidelity cost (:362-431): 10 (1-F)^2 + 5 (1-F11)^2 + 2 (1-p)^2 in
-    % units, + time_weight x t_gate; 1e6 for NaN or F < 0.5."""
-    return float(compute_cost_batch({k: np.atleast_1d(metrics.get(k, 0.0)) for k in
-                                     ("avg_fidelity", "f11", "cz_phase_fidelity")},
-                                    np.atleast_1d(gate_time_us), time_weight)[0])
+    % units, + time_weight x t_gate; 1e6 for NaN or F < 0.5.  ``cost="process_fidelity"``:
+    10 (1-F_gate)^2 % + time_weight x t_gate on the gauge-invariant average gate fidelity."""
+    keys = ("avg_fidelity", "f11", "cz_phase_fidelity", "avg_gate_fidelity")
+    return float(compute_cost_batch({k: np.atleast_1d(metrics.get(k, np.nan)) for k in keys},
+                                    np.atleast_1d(gate_time_us), time_weight, cost)[0])
 
 
 def compute_cost_batch(metrics: Dict[str, np.ndarray], gate_time_us: np.ndarray,
-                       time_weight: float = 0.01) -> np.ndarray:
-    """compute_cost over arrays (one entry per candidate)."""
+                       time_weight: float = 0.01, cost: str = "reference") -> np.ndarray:
+    """compute_cost over arrays (one entry per candidate).
+
+    ``cost="reference"`` (default) is the reference's cost, whose noisy avg F and phase
+    fidelity come from the eigenvector-phase penalty and so depend on the eigensolver's
+    gauge (RYD_STATUS_GAUGE_UNSTABLE); ``cost="process_fidelity"`` uses the average gate
+    fidelity to CZ up to local Z phases (noise_models.gate_fidelity), a continuous
+    function of the gate's map."""
+    t = time_weight * np.asarray(gate_time_us, dtype=float)
+    if cost == "process_fidelity":
+        fg = np.asarray(metrics["avg_gate_fidelity"], dtype=float)
+        c = 10.0 * ((1.0 - fg) * 100.0) ** 2 + t
+        return np.where(np.isnan(fg) | (fg < 0.50), FAIL_COST, c)
+    if cost != "reference":
+        raise ValueError(f"Unknown cost {cost!r}: use one of {COST_KINDS}")
     f = np.asarray(metrics["avg_fidelity"], dtype=float)
     f11 = np.asarray(metrics["f11"], dtype=float)
     p = np.asarray(metrics["cz_phase_fidelity"], dtype=float)
-    cost = (10.0 * ((1.0 - f) * 100.0) ** 2 + 5.0 * ((1.0 - f11) * 100.0) ** 2
-            + 2.0 * ((1.0 - p) * 100.0) ** 2 + time_weight * np.asarray(gate_time_us, dtype=float))
+    c = (10.0 * ((1.0 - f) * 100.0) ** 2 + 5.0 * ((1.0 - f11) * 100.0) ** 2
+         + 2.0 * ((1.0 - p) * 100.0) ** 2 + t)
     bad = np.isnan(f) | np.isnan(f11) | np.isnan(p) | (f < 0.50)
-    return np.where(bad, FAIL_COST, cost)
+    return np.where(bad, FAIL_COST, c)
 
 
 METRIC_KEYS = ("controlled_phase_deg", "phase_error_deg", "cz_phase_fidelity", "f00", "f01", "f10",
                "f11", "avg_fidelity", "gate_time_us", "V_over_Omega", "Omega_MHz")
+# carried when the evaluator provides them (the GPU evaluator does): the gauge-invariant
+# fidelities and the gauge flag of the reference penalty (1.0 = flagged)
+EXTRA_METRIC_KEYS = ("process_fidelity", "avg_gate_fidelity", "gauge_unstable")
 
 
 def extract_metrics(result) -> Dict[str, float]:
@@ -205,12 +230,16 @@ def extract_metrics_batch(br) -> Dict[str, np.ndarray]:
     c = br.batch.cols
     cp = br.controlled_phase
     err = np.minimum(np.abs(cp - np.pi), np.abs(cp + np.pi))
+    nan = np.full(br.n, np.nan)
     return {"controlled_phase_deg": np.degrees(cp), "phase_error_deg": np.degrees(err),
             "cz_phase_fidelity": br.cz_phase_fidelity.copy(),
             "f00": br.fidelities[:, 0].copy(), "f01": br.fidelities[:, 1].copy(),
             "f10": br.fidelities[:, 2].copy(), "f11": br.fidelities[:, 3].copy(),
             "avg_fidelity": br.avg_fidelity.copy(), "gate_time_us": c["tau_total"] * 1e6,
-            "V_over_Omega": c["V_over_Omega"].copy(), "Omega_MHz": c["Omega"] / (2 * np.pi * 1e6)}
+            "V_over_Omega": c["V_over_Omega"].copy(), "Omega_MHz": c["Omega"] / (2 * np.pi * 1e6),
+            "process_fidelity": nan.copy() if br.process_fidelity is None else br.process_fidelity.copy(),
+            "avg_gate_fidelity": nan.copy() if br.avg_gate_fidelity is None else br.avg_gate_fidelity.copy(),
+            "gauge_unstable": br.gauge_unstable.astype(float)}
 
 
 # ---------------------------------------------------------------------------
@@ -347,37 +376,48 @@ def _noise_hash(noise: NoiseSourceConfig) -> str:
 # ---------------------------------------------------------------------------
 
 def default_batch_evaluator(simulation_inputs, n: int, include_noise: bool, overrides: Dict[str, Any],
+                            *, process_fidelity: bool = False, gauge_copies: int = OPT_GAUGE_COPIES,
                             **apparatus) -> Tuple[Dict[str, np.ndarray], np.ndarray]:
     """One GPU pass over n candidates -> (metrics arrays, ok mask).  The metrics
-    dict also carries the derived batch under "_batch" (noise breakdowns)."""
+    dict also carries the derived batch under "_batch" (noise breakdowns).
+    ``process_fidelity``: also the gauge-invariant fidelities (one more engine pass for
+    the qubit coherences of noisy points); the gauge check of the reference penalty is
+    then skipped (the cost does not read it).  ``gauge_copies``: its probes otherwise."""
     from .simulation import simulate_CZ_gate_batch
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
         br = simulate_CZ_gate_batch(simulation_inputs, n, include_noise=include_noise,
-                                    overrides=overrides, **apparatus)
+                                    overrides=overrides, process_fidelity=process_fidelity,
+                                    gauge_check=not process_fidelity and gauge_copies > 0,
+                                    gauge_copies=gauge_copies, **apparatus)
     m = extract_metrics_batch(br)
     m["_batch"] = br.batch
     return m, br.ok
 
 
-def _evaluate_rows(evaluator, si, X_over: Dict[str, Any], n: int, include_noise: bool, apparatus_rows):
+def _evaluate_rows(evaluator, si, X_over: Dict[str, Any], n: int, include_noise: bool, apparatus_rows,
+                   **ev_kw):
     """Evaluate a population; if the whole batch raises (the reference's per-call
     exception path), fall back to one candidate at a time so only the failing
-    candidates get the failure cost."""
+    candidates get the failure cost.  ``ev_kw`` (e.g. process_fidelity=True) goes to
+    the evaluator only when given, so evaluators without those keywords still work."""
     try:
-        return evaluator(si, n, include_noise, X_over, **apparatus_rows)
+        return evaluator(si, n, include_noise, X_over, **ev_kw, **apparatus_rows)
     except Exception:
-        mets = {k: np.full(n, np.nan) for k in METRIC_KEYS}
+        mets = {k: np.full(n, np.nan) for k in METRIC_KEYS + EXTRA_METRIC_KEYS}
         ok = np.zeros(n, bool)
         for i in range(n):
             sub = {k: (v[i:i + 1] if np.ndim(v) > 0 else v) for k, v in X_over.items()}
             app = {k: (v[i:i + 1] if np.ndim(v) > 0 else v) for k, v in apparatus_rows.items()}
             try:
-                m, o = evaluator(si, 1, include_noise, sub, **app)
+                m, o = evaluator(si, 1, include_noise, sub, **ev_kw, **app)
             except Exception:
                 continue
             for k in METRIC_KEYS:
                 mets[k][i] = m[k][0]
+            for k in EXTRA_METRIC_KEYS:
+                if k in m:
+                    mets[k][i] = m[k][0]
             ok[i] = o[0]
         return mets, ok
 
@@ -401,6 +441,15 @@ class OptimizationResult:
     all_variants: Dict[str, Any] = field(default_factory=dict)
     cache_hits: int = 0
     n_batches: int = 0          # engine passes (new: one per DE generation / polish step)
+    cost: str = "reference"     # the cost minimised (COST_KINDS)
+    n_simulated: int = 0        # candidates evaluated by the engine (cache misses)
+    gauge_flagged: int = 0      # of those, noisy points whose reference penalty was gauge-flagged
+
+    @property
+    def gauge_flagged_fraction(self) -> float:
+        """Fraction of simulated candidates whose reference phase penalty (and so the
+        reference cost) depends on the eigensolver's gauge; a lower bound (4 probes)."""
+        return self.gauge_flagged / self.n_simulated if self.n_simulated else 0.0
 
     def __repr__(self) -> str:
         m = self.best_metrics
@@ -413,7 +462,8 @@ class OptimizationResult:
                 ("Gate time", f"{m.get('gate_time_us', 0):.3f} us"), ("V/Omega", f"{m.get('V_over_Omega', 0):.1f}"),
                 ("Omega/2pi", f"{m.get('Omega_MHz', 0):.3f} MHz"), ("Evaluations", f"{self.n_evaluations}"),
                 ("Engine batches", f"{self.n_batches}"), ("Runtime", f"{self.runtime_s:.1f} s"),
-                ("Cache hits", f"{self.cache_hits}")]
+                ("Cache hits", f"{self.cache_hits}"), ("Cost", self.cost),
+                ("Gauge-flagged", f"{self.gauge_flagged} of {self.n_simulated} simulated")]
         out = ["=" * 70, f"  CZ Gate Optimisation Result -- {self.protocol}", "=" * 70]
         out += [f"  {k + ':':18s}{v}" for k, v in rows]
         out += ["-" * 70, "  Optimal parameters:"]
@@ -440,14 +490,20 @@ def optimize_cz_gate(protocol: str, apparatus: ApparatusConstraints, include_noi
                      bounds: Optional[list] = None, x0: Optional[np.ndarray] = None,
                      cache: Optional[SimulationCache] = None, cache_path: Optional[str] = None,
                      strategy: str = "standard", variant: Optional[str] = None, verbose: bool = True,
-                     vectorized: bool = True, evaluator: Optional[Callable] = None) -> OptimizationResult:
+                     vectorized: bool = True, evaluator: Optional[Callable] = None,
+                     cost: str = "reference") -> OptimizationResult:
     """Differential-evolution search of the protocol parameters (RG/optimize_cz_gate.py:786-990).
 
     Extra keywords: ``vectorized`` (default True: one engine pass per DE generation,
     scipy's deferred updating; False: one candidate per call, the reference's
-    immediate updating) and ``evaluator`` (the batched metrics function, default
-    the GPU engine; tests inject the CPU oracle)."""
+    immediate updating), ``evaluator`` (the batched metrics function, default
+    the GPU engine; tests inject the CPU oracle) and ``cost`` ("reference", the
+    default, or "process_fidelity": the gauge-invariant average gate fidelity, see
+    compute_cost_batch).  The result reports how many simulated candidates had a
+    gauge-flagged reference penalty (``gauge_flagged``)."""
     pn = _normalise(protocol)
+    if cost not in COST_KINDS:
+        raise ValueError(f"Unknown cost {cost!r}: use one of {COST_KINDS}")
     is_bb = pn in ("jp_bangbang", "jp", "jandura_pupillo")
     excitation = apparatus.make_excitation_config(pol_purity=0.99 if include_noise else 1.0)
     noise = noise_config if noise_config is not None else (
@@ -472,7 +528,7 @@ def optimize_cz_gate(protocol: str, apparatus: ApparatusConstraints, include_noi
         r = _optimize_single_variant(pn, nseg, excitation, noise, apparatus, include_noise, time_weight,
                                      maxiter, popsize, tol, seed, bounds, x0, cache, strategy, verbose,
                                      optimize_spacing, spacing_bounds, vectorized,
-                                     evaluator or default_batch_evaluator)
+                                     evaluator or default_batch_evaluator, cost)
         r.discrete_variant = name
         results[name] = r
         if verbose:
@@ -497,7 +553,7 @@ class _Objective:
 
     def __init__(self, space: _Param, excitation, noise, apparatus: ApparatusConstraints,
                  include_noise: bool, time_weight: float, cache: SimulationCache, optimize_spacing: bool,
-                 evaluator: Callable, verbose: bool):
+                 evaluator: Callable, verbose: bool, cost: str = "reference"):
         self.space, self.excitation, self.noise = space, excitation, noise
         self.apparatus, self.include_noise, self.time_weight = apparatus, include_noise, time_weight
         self.cache, self.optimize_spacing, self.evaluator, self.verbose = cache, optimize_spacing, evaluator, verbose
@@ -506,6 +562,9 @@ class _Objective:
         self.n_eval = 0
         self.n_hits = 0
         self.n_batches = 0
+        self.n_sim = 0
+        self.n_flagged = 0
+        self.cost = cost
         self.best = np.inf
         self.d = len(space.names)
 
@@ -516,7 +575,9 @@ class _Objective:
 
     def key(self, prot: np.ndarray, sf: float) -> str:
         h = self.app_hash if not self.optimize_spacing else f"{self.app_hash}_sf{sf:.6f}"
-        return self.cache.make_key(self.space.cache_protocol, prot.tolist(), f"{h}_n{self.noise_hash}")
+        # the reference cost keeps the reference's key; another cost must not share entries
+        tag = "" if self.cost == "reference" else f"_{self.cost}"
+        return self.cache.make_key(self.space.cache_protocol, prot.tolist(), f"{h}_n{self.noise_hash}{tag}")
 
     def evaluate(self, X: np.ndarray) -> Tuple[np.ndarray, List[Optional[Dict]]]:
         """X (S, D) -> (costs (S,), metrics dict or None per member)."""
@@ -539,14 +600,19 @@ class _Objective:
             idx = np.array(miss)
             si, over = self.space.inputs(prot[idx], self.excitation, self.noise)
             app = self.apparatus.simulate_kwargs(spacing_factor=sf[idx] if self.optimize_spacing else None)
-            m, ok = _evaluate_rows(self.evaluator, si, over, idx.size, self.include_noise, app)
+            ev_kw = {"process_fidelity": True} if self.cost == "process_fidelity" else {}
+            m, ok = _evaluate_rows(self.evaluator, si, over, idx.size, self.include_noise, app, **ev_kw)
             self.n_batches += 1
-            c = compute_cost_batch(m, m["gate_time_us"], self.time_weight)
+            self.n_sim += idx.size
+            if "gauge_unstable" in m:
+                self.n_flagged += int(np.nansum(np.asarray(m["gauge_unstable"], dtype=float)[ok] > 0))
+            c = compute_cost_batch(m, m["gate_time_us"], self.time_weight, self.cost)
             c = np.where(ok, c, FAIL_COST)
             for j, i in enumerate(miss):
                 costs[i] = c[j]
                 if ok[j]:
                     mets[i] = {k: float(m[k][j]) for k in METRIC_KEYS}
+                    mets[i].update({k: float(m[k][j]) for k in EXTRA_METRIC_KEYS if k in m})
                     self.cache[keys[i]] = (float(c[j]), mets[i])
                 if c[j] < self.best:
                     self.best = c[j]
@@ -574,7 +640,8 @@ def _run_de(obj: _Objective, bounds, x0, maxiter, popsize, tol, seed, vectorized
 
 def _optimize_single_variant(pn, n_segments, excitation, noise, apparatus, include_noise, time_weight,
                              maxiter, popsize, tol, seed, bounds, x0, cache, strategy, verbose,
-                             optimize_spacing, spacing_bounds, vectorized, evaluator) -> OptimizationResult:
+                             optimize_spacing, spacing_bounds, vectorized, evaluator,
+                             cost: str = "reference") -> OptimizationResult:
     """DE for one discrete variant (:993-1324)."""
     space = _param_space(pn, n_segments)
     names = list(space.names)
@@ -585,7 +652,7 @@ def _optimize_single_variant(pn, n_segments, excitation, noise, apparatus, inclu
         x0 = np.append(x0, apparatus.spacing_factor)
         names.append("spacing_factor")
     obj = _Objective(space, excitation, noise, apparatus, include_noise, time_weight, cache,
-                     optimize_spacing, evaluator, verbose)
+                     optimize_spacing, evaluator, verbose, cost)
     t0 = time.time()
     if strategy == "two_phase" and space.kind == "smooth_jp":
         # phase 1: omega_tau (and spacing) only, the other shape parameters at x0 (:1184-1241)
@@ -599,7 +666,7 @@ def _optimize_single_variant(pn, n_segments, excitation, noise, apparatus, inclu
             return full
 
         p1 = _Objective(space, excitation, noise, apparatus, include_noise, time_weight, cache,
-                        optimize_spacing, evaluator, verbose)
+                        optimize_spacing, evaluator, verbose, cost)
         fn = (lambda y: p1.evaluate(expand(np.asarray(y).T))[0]) if vectorized else \
              (lambda y: float(p1.evaluate(expand(np.asarray(y)))[0][0]))
         extra = dict(vectorized=True, updating="deferred") if vectorized else {}
@@ -608,6 +675,8 @@ def _optimize_single_variant(pn, n_segments, excitation, noise, apparatus, inclu
         obj.n_eval += p1.n_eval
         obj.n_hits += p1.n_hits
         obj.n_batches += p1.n_batches
+        obj.n_sim += p1.n_sim
+        obj.n_flagged += p1.n_flagged
         x0 = expand(r1.x)[0]
         ot = r1.x[0]
         bounds = [(max(bounds[0][0], ot * 0.7), min(bounds[0][1], ot * 1.3))] + bounds[1:]
@@ -630,7 +699,8 @@ def _optimize_single_variant(pn, n_segments, excitation, noise, apparatus, inclu
                and final.get("phase_error_deg", 999) < 10.0)
     return OptimizationResult(success=success, protocol=pn, best_params=np.asarray(de.x), param_names=names,
                               best_cost=float(de.fun), best_metrics=final, n_evaluations=obj.n_eval,
-                              runtime_s=runtime, cache_hits=obj.n_hits, n_batches=obj.n_batches)
+                              runtime_s=runtime, cache_hits=obj.n_hits, n_batches=obj.n_batches, cost=cost,
+                              n_simulated=obj.n_sim, gauge_flagged=obj.n_flagged)
 
 
 def run_baseline(protocol: str, apparatus: ApparatusConstraints, include_noise: bool = False,
@@ -658,6 +728,6 @@ def run_baseline(protocol: str, apparatus: ApparatusConstraints, include_noise: 
     return metrics
 
 
-__all__ = ["ApparatusConstraints", "SimulationCache", "compute_cost", "compute_cost_batch",
+__all__ = ["ApparatusConstraints", "SimulationCache", "compute_cost", "compute_cost_batch", "COST_KINDS",
            "extract_metrics", "extract_metrics_batch", "warm_start_bounds", "OptimizationResult",
            "optimize_cz_gate", "run_baseline", "default_batch_evaluator"]

@@ -101,6 +101,9 @@ def _inputs(protocol: str, params: Dict[str, Any]):
     return JPSimulationInputs(excitation=exc, noise=noise)
 
 
+SWEEP_GAUGE_COPIES = 4
+
+
 def _batch_call(protocol: str, rows: List[Dict[str, Any]], devices=None):
     """One simulate_CZ_gate_batch over rows that share every non-array setting."""
     from .simulation import simulate_CZ_gate_batch
@@ -118,8 +121,9 @@ def _batch_call(protocol: str, rows: List[Dict[str, Any]], devices=None):
         for d in dsts:
             ov[d] = vals
     si = _inputs(protocol, p0)
+    # 4 gauge probes instead of 16: the flag stays a proof where set
     return simulate_CZ_gate_batch(si, n, include_noise=bool(p0.get("include_noise", True)), overrides=ov,
-                                  devices=devices, **kw)
+                                  devices=devices, gauge_copies=SWEEP_GAUGE_COPIES, **kw)
 
 
 def _fails_like_reference(protocol: str, row: Dict[str, Any]) -> Optional[str]:

@@ -231,6 +231,12 @@ class SimulationResult:
     H2: Any = None
     c_ops: List = None
     hs: Any = None
+    # not in the reference's record: the gauge-invariant process / average gate fidelity
+    # to CZ up to local Z phases (simulate_CZ_gate(..., process_fidelity=True)), None if
+    # not requested; unlike avg_fidelity's noisy phase penalty they do not depend on the
+    # eigensolver's gauge
+    process_fidelity: Optional[float] = None
+    avg_gate_fidelity: Optional[float] = None
 
     def __post_init__(self):
         for k in ("magic_wavelength_analysis", "noise_breakdown", "pulse_info", "results"):
@@ -275,6 +281,10 @@ class BatchResult:
     is_mixed: np.ndarray
     states: Optional[np.ndarray] = None   # rho (n,4,9,9) or kets (n,4,9) (complex)
     kernel_ms: float = 0.0
+    # gauge-invariant figures of merit (``process_fidelity=True``; NaN otherwise, and for
+    # dim 4 Lindblad points): process / average gate fidelity to CZ up to local Z phases
+    process_fidelity: Optional[np.ndarray] = None
+    avg_gate_fidelity: Optional[np.ndarray] = None
     timings: Dict[str, float] = field(default_factory=dict)   # host wall ms per stage
 
     @property
@@ -320,8 +330,13 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                            trap_laser_on: bool = True, overrides: Optional[Dict[str, Any]] = None,
                            phase_penalty: str = "reference", eigh=None, return_states: bool = False,
                            devices=None, method: str = "chebyshev", gauge_check: bool = True,
-                           gauge_copies: Optional[int] = None) -> BatchResult:
-    """Evaluate many simulate_CZ_gate points in one GPU pass (see module doc)."""
+                           gauge_copies: Optional[int] = None, process_fidelity: bool = False) -> BatchResult:
+    """Evaluate many simulate_CZ_gate points in one GPU pass (see module doc).
+
+    ``process_fidelity``: also compute the gauge-invariant process fidelity and average
+    gate fidelity to CZ up to local Z phases (noise_models.gate_fidelity) -- from the
+    kets for noise-free points, from the Lindblad state plus one ryd_run_coherences pass
+    (the 6 qubit coherences) for noisy dim-3 points."""
     if hilbert_space_dim not in (3, 4):
         raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
     dim = hilbert_space_dim
@@ -346,6 +361,8 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     pops = np.zeros((nn, 4))
     cp = np.full(nn, np.nan)
     pen = np.ones(nn)
+    fpro = np.full(nn, np.nan)
+    fgate = np.full(nn, np.nan)
     status = b.status_bits.copy() if b.status_bits is not None else np.zeros(nn, np.uint32)
     states = None
     if return_states:
@@ -359,9 +376,17 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
         if idx.size == 0:
             continue
         t0 = time.perf_counter()
-        r = eng.run(E.pack_params(b, idx), key, evol, shape=shape,
-                    method=method if dim == 3 else "chebyshev", dim=dim)
+        prm = E.pack_params(b, idx)
+        r = eng.run(prm, key, evol, shape=shape, method=method if dim == 3 else "chebyshev", dim=dim)
+        coh = None
+        if process_fidelity and evol == "lindblad" and dim == 3:
+            coh, cst = eng.run_coherences(prm, key, shape=shape)
+            status[idx] |= cst
         engine_s += time.perf_counter() - t0
+        if process_fidelity and (evol == "ket" or coh is not None):
+            from . import noise_models as NM
+            S = NM.ket_maps(r.kets(), dim) if evol == "ket" else NM.assemble_maps(r.state, coh)
+            fpro[idx], fgate[idx] = NM.gate_fidelity(S)
         kms += r.kernel_ms
         status[idx] |= r.status
         P = r.populations()
@@ -399,7 +424,8 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                "epilogue_ms": (t_end - t_derived - engine_s) * 1e3, "total_ms": (t_end - t_start) * 1e3}
     return BatchResult(batch=b, avg_fidelity=avg, fidelities=fids, populations=pops,
                        controlled_phase=cp, cz_phase_fidelity=pen, status=status,
-                       is_mixed=~ket_mask, states=out_states, kernel_ms=kms, timings=timings)
+                       is_mixed=~ket_mask, states=out_states, kernel_ms=kms, timings=timings,
+                       process_fidelity=fpro, avg_gate_fidelity=fgate)
 
 
 def noise_breakdown_row(b: PH.DerivedBatch, i: int, n_collapse_ops: Optional[int] = None) -> Dict[str, Any]:
@@ -445,9 +471,11 @@ def simulate_CZ_gate(
     tweezer_wavelength_nm: float = None, temperature: float = 2e-6, B_field: float = 1e-4,
     NA: float = 0.5, spacing_factor: float = 2.8, include_noise: bool = True,
     background_loss_rate_hz: float = None, trap_laser_on: bool = True, verbose: bool = False,
-    return_dataclass: bool = True, *, eigh=None,
+    return_dataclass: bool = True, *, eigh=None, process_fidelity: bool = False,
 ) -> Union[SimulationResult, Dict]:
-    """Drop-in for RG/simulation.py:2534 (same arguments, same outputs) on the GPU engine."""
+    """Drop-in for RG/simulation.py:2534 (same arguments, same outputs) on the GPU engine.
+    ``process_fidelity=True`` also fills the gauge-invariant ``process_fidelity`` and
+    ``avg_gate_fidelity`` (dim 3; noise-free points in dim 4)."""
     if config is None:
         config = AtomicConfiguration(species=species, qubit_0=qubit_0, qubit_1=qubit_1,
                                      n_rydberg=n_rydberg, L_rydberg="S")
@@ -458,7 +486,7 @@ def simulate_CZ_gate(
         tweezer_wavelength_nm=tweezer_wavelength_nm, temperature=temperature, B_field=B_field,
         NA=NA, spacing_factor=spacing_factor, include_noise=include_noise,
         background_loss_rate_hz=background_loss_rate_hz, trap_laser_on=trap_laser_on,
-        phase_penalty="reference", eigh=eigh, return_states=True)
+        phase_penalty="reference", eigh=eigh, return_states=True, process_fidelity=process_fidelity)
     if not br.ok[0]:
         raise RuntimeError(f"GPU engine failed for this point (status bits {int(br.status[0])})")
     b = br.batch
@@ -518,6 +546,9 @@ def simulate_CZ_gate(
         qubit_1=config.qubit_1, temperature_K=temperature, B_field_T=B_field,
         delta_zeeman=c["delta_zeeman"], delta_stark=c["delta_stark"] if trap_laser_on else 0.0,
         trap_laser_on=trap_laser_on, results=results, H1=H1, H2=H2, c_ops=c_ops, hs=hs)
+    if process_fidelity and np.isfinite(br.process_fidelity[0]):
+        rd.update(process_fidelity=float(br.process_fidelity[0]),
+                  avg_gate_fidelity=float(br.avg_gate_fidelity[0]))
     if verbose:
         print(f"  V/Ω = {rd['V_over_Omega']:.1f}; τ_total = {rd['tau_total'] * 1e6:.3f} µs; "
               f"avg F = {avg:.6f}")

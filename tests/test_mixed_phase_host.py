@@ -150,3 +150,21 @@ def test_private_lapack_pool_is_bit_identical():
         for x in range(4):
             w, U = sla.eigh(expand_like_host(st[:, 4 * i + x]))
             assert np.angle(U[IDX[x], int(np.argmax(w))]) == ph4[i, x]
+
+
+def test_lapack_pool_loads_once_per_process():
+    """ryd_lapack_pool attempts loading once: later calls, whatever copies they
+    ask for, return the first outcome and never dlmopen again; copies are capped at 8."""
+    import ctypes
+    import glob
+    import os
+    import scipy
+    first = N.scipy_lapack_pool(4)
+    assert N.scipy_lapack_pool(16) == first            # Python cache: no reload
+    libs = sorted(glob.glob(os.path.join(os.path.dirname(os.path.dirname(scipy.__file__)), "scipy.libs",
+                                         "libscipy_openblas*.so")))
+    got = ctypes.c_int(-1)
+    rc = N.load().ryd_lapack_pool(N.scipy_zheevr(), libs[0].encode(), b"scipy_zheevr_",
+                                  b"scipy_openblas_set_num_threads", 16, ctypes.byref(got))
+    assert got.value == first and (rc == 0) == (first >= 2)   # library cache: same outcome
+    assert first <= 8

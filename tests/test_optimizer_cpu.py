@@ -27,6 +27,47 @@ def test_compute_cost_matches_reference_formula():
     assert c[0] == pytest.approx(want) and c[1] == 1e6
 
 
+def test_process_fidelity_cost():
+    """cost="process_fidelity": 10 (1-F_gate)^2 % + time weight, failures 1e6; an unknown
+    cost kind is an error."""
+    m = dict(avg_gate_fidelity=np.array([0.995, 0.4, np.nan]))
+    c = OC.compute_cost_batch(m, np.array([0.4, 0.1, 0.1]), 0.01, "process_fidelity")
+    assert c[0] == pytest.approx(10 * 0.5 ** 2 + 0.004) and c[1] == c[2] == 1e6
+    assert OC.compute_cost(dict(avg_gate_fidelity=0.995), 0.4, cost="process_fidelity") == pytest.approx(c[0])
+    with pytest.raises(ValueError):
+        OC.compute_cost_batch(m, np.zeros(3), cost="bogus")
+
+
+def test_objective_counts_gauge_flags_and_tags_cache_keys():
+    """The DE objective counts gauge-flagged simulated candidates (reported by
+    OptimizationResult) and keys a non-reference cost apart from the reference's keys."""
+    calls = []
+
+    def fake(si, n, include_noise, overrides, process_fidelity=False, **app):
+        calls.append(process_fidelity)
+        m = {k: np.full(n, 0.99) for k in OC.METRIC_KEYS}
+        m["gauge_unstable"] = (np.arange(n) % 2).astype(float)
+        m["avg_gate_fidelity"] = np.full(n, 0.98)
+        return m, np.ones(n, bool)
+
+    app = OC.ApparatusConstraints()
+    space = OC._param_space("lp")
+    exc = app.make_excitation_config()
+    noise = app.make_full_noise()
+    for cost in ("reference", "process_fidelity"):
+        obj = OC._Objective(space, exc, noise, app, True, 0.01, OC.SimulationCache(), False, fake, False, cost)
+        X = np.array([[0.3, 4.0], [0.31, 4.1], [0.32, 4.2], [0.33, 4.3]])
+        costs, mets = obj.evaluate(X)
+        assert obj.n_sim == 4 and obj.n_flagged == 2
+        assert calls[-1] == (cost == "process_fidelity")
+        key = obj.key(X[0], app.spacing_factor)
+        assert ("_process_fidelity|" in key) == (cost == "process_fidelity")
+        assert mets[0]["avg_gate_fidelity"] == 0.98
+        want = OC.compute_cost_batch({"avg_fidelity": [0.99], "f11": [0.99], "cz_phase_fidelity": [0.99],
+                                      "avg_gate_fidelity": [0.98]}, mets[0]["gate_time_us"], 0.01, cost)[0]
+        assert costs[0] == pytest.approx(want)
+
+
 def test_cache_keys_and_persistence(tmp_path):
     c = OC.SimulationCache(precision=4)
     k = c.make_key("smooth_jp", [10.09123456, 0.311], "abc")

@@ -94,3 +94,29 @@ def test_depolarised_cz_known_answer():
     assert pm.pauli_probs[0, 0] == pytest.approx(1 - 15 * p / 16)
     assert pm.process_fidelity[0] == pytest.approx(1 - 15 * p / 16)
     assert pm.avg_gate_fidelity[0] == pytest.approx((4 * (1 - 15 * p / 16) + 1) / 5)
+
+
+def test_ket_maps_and_gate_fidelity_of_ideal_cz():
+    """noise_models.ket_maps + gate_fidelity (the gauge-invariant figure of merit on
+    BatchResult / SimulationResult): an exact CZ with arbitrary local Z phases and a
+    global phase has process fidelity 1; a swap of the |11> sign (identity) has 0.25."""
+    rng = np.random.default_rng(5)
+    for d in (3, 4):
+        a, b, g = rng.uniform(-np.pi, np.pi, 3)
+        q = [0, 1, d, d + 1]
+        psi = np.zeros((2, 4, d * d), complex)
+        u = np.exp(1j * g) * np.array([1, np.exp(1j * b), np.exp(1j * a), -np.exp(1j * (a + b))])
+        for x in range(4):
+            psi[0, x, q[x]] = u[x]
+            psi[1, x, q[x]] = 1.0
+        fpro, favg = NM.gate_fidelity(NM.ket_maps(psi, d))
+        np.testing.assert_allclose(fpro, [1.0, 0.25], atol=1e-12)
+        np.testing.assert_allclose(favg, [1.0, 0.4], atol=1e-12)
+
+
+def test_gate_fidelity_equals_analyse_on_noisy_map(noisy_map):
+    S = noisy_map[None]
+    fpro, favg = NM.gate_fidelity(S)
+    pm = NM.analyse(S)
+    np.testing.assert_array_equal(fpro, pm.process_fidelity)
+    np.testing.assert_array_equal(favg, pm.avg_gate_fidelity)

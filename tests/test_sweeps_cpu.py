@@ -13,9 +13,10 @@ class _Fake:
     def __init__(self):
         self.calls = []
 
-    def __call__(self, si, n, include_noise=True, overrides=None, devices=None, **kw):
+    def __call__(self, si, n, include_noise=True, overrides=None, devices=None, gauge_copies=None, **kw):
         from noisyquantumsimulator_amd import physics as PH
-        self.calls.append(dict(si=si, n=n, include_noise=include_noise, overrides=overrides, kw=kw))
+        self.calls.append(dict(si=si, n=n, include_noise=include_noise, overrides=overrides, kw=kw,
+                               gauge_copies=gauge_copies))
         b = PH.derive_batch(si, n, include_noise=include_noise, overrides=overrides, **kw)
         F = np.tile(np.arange(n, dtype=float)[:, None] / 100, (1, 4))
         return SIM.BatchResult(batch=b, avg_fidelity=F.mean(1), fidelities=F, populations=F,
@@ -34,6 +35,7 @@ def test_defaults_quirks_and_nan_rows(monkeypatch):
     assert np.all(np.isfinite(r.fidelities_lp[[0, 2]])) and np.all(np.isfinite(r.gate_times_jp[[0, 2]]))
     assert len(fake.calls) == 2                     # one batch per protocol
     lp, jp = fake.calls
+    assert lp["gauge_copies"] == RS.SWEEP_GAUGE_COPIES == 4    # fewer gauge probes
     assert lp["n"] == 2 and type(lp["si"]).__name__ == "LPSimulationInputs" and lp["si"].pulse_shape == "square"
     assert type(jp["si"]).__name__ == "JPSimulationInputs"
     np.testing.assert_allclose(lp["overrides"]["Delta_e"], [2 * np.pi * 1e9, 2 * np.pi * 5e9])
