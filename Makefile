@@ -16,10 +16,16 @@ resource-usage: $(SRC)
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -o /tmp/ryd_ru.so $(SRC) 2>&1 | \
 	  grep -E "Function Name|VGPRs:|AGPRs|ScratchSize|Occupancy|SGPRs:" 
 
+ASM ?= /tmp/ryd_engine.s
+
 asm: $(SRC)
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC --cuda-device-only -S -o /tmp/ryd_engine.s $(SRC)
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC --cuda-device-only -S -o $(ASM) $(SRC)
+
+# the inline-asm DPP groups: no VALU write within 2 wait states of a DPP read
+check-dpp: asm
+	python3 tools/check_dpp_hazards.py $(ASM)
 
 clean:
 	rm -f $(SO)
 
-.PHONY: all clean resource-usage asm
+.PHONY: all clean resource-usage asm check-dpp

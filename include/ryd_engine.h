@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RYD_ABI_VERSION 3
+#define RYD_ABI_VERSION 4
 
 /* ---- return codes ---- */
 #define RYD_OK              0
@@ -355,9 +355,11 @@ int ryd_lapack_pool(void* ref_zheevr, const char* path, const char* zheevr_symbo
  * threads.  out[0] = n_slots, out[1] = host pack ms, out[2] = host unpack ms,
  * out[3] = call wall ms; then per slot RYD_TL_SLOT doubles: device id, H2D start,
  * kernel start, kernel end, D2H end (ms, HIP events, relative to the start of the first
- * slot on the same device), points.  cap >= 4 + RYD_TL_SLOT * n_slots. */
+ * slot on the same device), points, then host ms since the call began at which the
+ * slot's kernel was enqueued and at which the host began waiting for the slot (every
+ * slot is enqueued before the first wait).  cap >= 4 + RYD_TL_SLOT * n_slots. */
 #define RYD_TL_HEAD 4
-#define RYD_TL_SLOT 6
+#define RYD_TL_SLOT 8
 int ryd_last_timeline(ryd_handle* h, double* out, int64_t cap);
 
 /* Region timing on a slot's stream: ryd_mark(h, slot, 0) ... launches ...

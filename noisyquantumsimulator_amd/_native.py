@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RYD_ENGINE_LIB") or os.path.join(_HERE, "libryd_engine.so")
 
 # keep in sync with include/ryd_engine.h
-RYD_ABI_VERSION = 3
+RYD_ABI_VERSION = 4
 RYD_OK = 0
 PROTO = {"lp_square": 0, "lp_shaped": 1, "bangbang": 2, "smooth_jp": 3}
 EVOL = {"lindblad": 0, "ket": 1}
@@ -51,7 +51,7 @@ TS = dict(MEAN_JUMPS=0, FRAC_JUMPED=1, MAX_JUMPS=2, TRACE=3, QUBIT_POP=4, ITER_U
 T_NSUMMARY = 10
 
 # ryd_last_timeline layout
-TL_HEAD, TL_SLOT = 4, 6
+TL_HEAD, TL_SLOT = 4, 8
 
 EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary_width", "ryd_lp_unsquared",
             "ryd_state_width", "ryd_device_count", "ryd_create", "ryd_destroy", "ryd_run_batch",

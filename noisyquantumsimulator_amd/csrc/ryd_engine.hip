@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -2337,30 +2338,86 @@ struct CopyTask {
   size_t bytes;
 };
 
-// memcpy a task list with up to host_threads() threads (serial below 1 MiB); rows
-// larger than 256 KiB are cut so the threads balance.
+// Persistent host worker pool for the staging copies: created on the first large copy
+// and kept for the life of the process (never joined: the workers sleep on a condition
+// variable), so a call pays a wake-up, not a thread creation per worker.  One job at a
+// time; the calling thread works on it too.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool(host_threads() - 1);    // leaked on purpose (no exit-time join)
+    return *p;
+  }
+  int workers() const { return (int)th_.size(); }
+  // run every task of `tasks` on the caller + up to `helpers` workers; returns when done
+  void run(const std::vector<CopyTask>& tasks, int helpers) {
+    std::lock_guard<std::mutex> one(call_mu_);
+    helpers = std::max(0, std::min(helpers, workers()));
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      tasks_ = &tasks;
+      next_.store(0);
+      want_ = helpers;
+      pending_ = helpers;
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain(tasks);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    tasks_ = nullptr;
+  }
+
+ private:
+  explicit HostPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this, i] { loop(i); });
+    for (auto& t : th_) t.detach();
+  }
+  void drain(const std::vector<CopyTask>& t) {
+    for (size_t i; (i = next_.fetch_add(1)) < t.size();) memcpy(t[i].dst, t[i].src, t[i].bytes);
+  }
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::vector<CopyTask>* t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= want_) continue;               // not needed for this job
+        t = tasks_;
+      }
+      drain(*t);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_;
+  const std::vector<CopyTask>* tasks_ = nullptr;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  int want_ = 0, pending_ = 0;
+};
+
+// memcpy a task list on the persistent pool (serial below 256 KiB); rows larger than
+// 128 KiB are cut so the threads balance.
 void parallel_copy(const std::vector<CopyTask>& in) {
   std::vector<CopyTask> tasks;
   size_t total = 0;
-  const size_t cut = 256 << 10;
+  const size_t cut = 128 << 10;
   for (const CopyTask& t : in) {
     total += t.bytes;
     for (size_t o = 0; o < t.bytes; o += cut)
       tasks.push_back({(char*)t.dst + o, (const char*)t.src + o, std::min(cut, t.bytes - o)});
   }
-  int nt = std::min<int64_t>(host_threads(), (int64_t)tasks.size());
-  if (total < (1u << 20) || nt <= 1) {
+  const int helpers = (int)std::min<int64_t>(host_threads() - 1, (int64_t)tasks.size() - 1);
+  if (total < (256u << 10) || helpers <= 0) {
     for (const CopyTask& t : tasks) memcpy(t.dst, t.src, t.bytes);
     return;
   }
-  std::atomic<size_t> next{0};
-  auto work = [&]() {
-    for (size_t i; (i = next.fetch_add(1)) < tasks.size();) memcpy(tasks[i].dst, tasks[i].src, tasks[i].bytes);
-  };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < nt; ++t) pool.emplace_back(work);
-  work();
-  for (auto& th : pool) th.join();
+  HostPool::get().run(tasks, helpers);
 }
 
 double host_ms_since(std::chrono::steady_clock::time_point t0) {
@@ -2414,9 +2471,9 @@ void release_slot_work(ryd_slot_work& w) {
 
 // Range-partition n points over the handle's devices (point i -> slot
 // floor(nd*i/n)), one stream each, no inter-device traffic.
-// Per slot, in order: pack the shard's parameter columns into the slot's pinned
-// staging buffer, enqueue H2D + `launch_fn(dp, cnt, ldp, off, dev_outs, dstat, stream)`;
-// then every slot's D2H into staging -- all enqueued before the first wait, so devices
+// Every slot's parameter columns are packed into its pinned staging buffer in one
+// parallel pass first; then per slot, in order, H2D + `launch_fn(dp, cnt, ldp, off,
+// dev_outs, dstat, stream)`; then every slot's D2H into staging -- all enqueued before the first wait, so devices
 // (and same-device slots) overlap -- then wait slot by slot and unpack staging into
 // the caller's strided buffers with host threads.  Device workspace and staging
 // persist in the handle.  Device times are the max over slots; the per-slot event
@@ -2435,6 +2492,7 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
     size_t o_par, o_st;
     std::vector<size_t> o_out;
     bool queued;
+    double t_enq = 0.0, t_wait = 0.0;    // host ms since the call began: kernel enqueued, wait began
   };
   std::vector<Part> parts(nd);
   kms = hms = dms = 0.0;
@@ -2446,6 +2504,9 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
         (void)hipStreamSynchronize(h->stream[k]);
       }
   };
+  // (1) partition + workspace for every slot, (2) pack every slot's parameter columns in
+  // ONE parallel pass, (3) enqueue H2D + kernel slot by slot: slot k+1's H2D no longer
+  // waits for slot k+1's pack behind slot k's enqueue.
   for (int k = 0; k < nd; ++k) {
     Part& P = parts[k];
     P.off = n * k / nd;
@@ -2463,26 +2524,36 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
     P.o_st = at;
     at = align256(at + sizeof(uint32_t) * P.cnt);
     hipError_t e = hipSetDevice(h->dev[k]);
+    if (e != hipSuccess) return fail(RYD_ERR_HIP, std::string("set device: ") + hipGetErrorString(e));
+    int rc = ensure_slot_work(h, k, at);
+    if (rc) return rc;
+  }
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<CopyTask> pack;
+    for (int k = 0; k < nd; ++k) {
+      const Part& P = parts[k];
+      if (P.cnt == 0) continue;
+      char* hb = (char*)h->work[k].hbuf;
+      for (int c = 0; c < RYD_NPARAM; ++c)
+        pack.push_back({hb + P.o_par + sizeof(double) * c * P.cnt, params + (int64_t)c * ld_params + P.off,
+                        sizeof(double) * P.cnt});
+    }
+    parallel_copy(pack);
+    pack_ms = host_ms_since(t0);
+  }
+  for (int k = 0; k < nd; ++k) {
+    Part& P = parts[k];
+    if (P.cnt == 0) continue;
+    hipError_t e = hipSetDevice(h->dev[k]);
     if (e != hipSuccess) {
       drain(k);
       return fail(RYD_ERR_HIP, std::string("set device: ") + hipGetErrorString(e));
-    }
-    int rc = ensure_slot_work(h, k, at);
-    if (rc) {
-      drain(k);
-      return rc;
     }
     ryd_slot_work& W = h->work[k];
     char* hb = (char*)W.hbuf;
     char* db = (char*)W.dbuf;
     hipStream_t s = h->stream[k];
-    const auto t0 = std::chrono::steady_clock::now();
-    std::vector<CopyTask> pack;
-    for (int c = 0; c < RYD_NPARAM; ++c)
-      pack.push_back({hb + P.o_par + sizeof(double) * c * P.cnt, params + (int64_t)c * ld_params + P.off,
-                      sizeof(double) * P.cnt});
-    parallel_copy(pack);
-    pack_ms += host_ms_since(t0);
     std::vector<double*> dout(no);
     for (int j = 0; j < no; ++j) dout[j] = (double*)(db + P.o_out[j]);
     e = hipEventRecord(W.ev[0], s);
@@ -2496,7 +2567,7 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
       return fail(RYD_ERR_HIP, std::string("h2d: ") + hipGetErrorString(e));
     }
     P.queued = true;
-    rc = launch_fn((const double*)(db + P.o_par), P.cnt, P.cnt, P.off, dout, (uint32_t*)(db + P.o_st), s);
+    int rc = launch_fn((const double*)(db + P.o_par), P.cnt, P.cnt, P.off, dout, (uint32_t*)(db + P.o_st), s);
     if (rc) {
       drain(k + 1);
       return rc;
@@ -2506,6 +2577,7 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
       drain(k + 1);
       return fail(RYD_ERR_HIP, std::string("event: ") + hipGetErrorString(e));
     }
+    P.t_enq = host_ms_since(t_call);
   }
   // D2Hs only after every slot's H2D: copies of one device's streams share its DMA
   // rings in submission order, so a D2H (waiting for its kernel) enqueued before the
@@ -2526,16 +2598,19 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
     }
   }
   hipError_t err = hipSuccess;
-  h->timeline.assign(4 + 6 * (size_t)nd, 0.0);
+  h->timeline.assign(RYD_TL_HEAD + RYD_TL_SLOT * (size_t)nd, 0.0);
   std::vector<hipEvent_t> origin(nd, nullptr);   // first slot's start event, per device
   for (int k = 0; k < nd; ++k) {
     Part& P = parts[k];
-    double* tl = &h->timeline[4 + 6 * (size_t)k];
+    double* tl = &h->timeline[RYD_TL_HEAD + RYD_TL_SLOT * (size_t)k];
     tl[0] = h->dev[k];
     tl[5] = (double)P.cnt;
     if (P.cnt == 0) continue;
     ryd_slot_work& W = h->work[k];
     (void)hipSetDevice(h->dev[k]);
+    P.t_wait = host_ms_since(t_call);
+    tl[6] = P.t_enq;
+    tl[7] = P.t_wait;
     hipError_t e = hipStreamSynchronize(h->stream[k]);
     if (e != hipSuccess) {
       err = e;

@@ -277,7 +277,7 @@ class Engine:
         for k in range(int(buf[0])):
             t = buf[N.TL_HEAD + N.TL_SLOT * k: N.TL_HEAD + N.TL_SLOT * (k + 1)]
             slots.append(dict(device=int(t[0]), h2d_start=t[1], kernel_start=t[2], kernel_end=t[3],
-                              d2h_end=t[4], points=int(t[5])))
+                              d2h_end=t[4], points=int(t[5]), host_enqueued=t[6], host_wait=t[7]))
         return dict(pack_ms=buf[1], unpack_ms=buf[2], wall_ms=buf[3], slots=slots)
 
     def run_coherences(self, params: np.ndarray, protocol: str, n_steps: Optional[int] = None,

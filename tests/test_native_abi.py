@@ -50,7 +50,7 @@ def test_library_loads_and_exports():
     lib = N.load()
     for sym in N.EXPORTED:
         assert hasattr(lib, sym), sym
-    assert lib.ryd_abi_version() == N.RYD_ABI_VERSION == 3
+    assert lib.ryd_abi_version() == N.RYD_ABI_VERSION == 4
     assert lib.ryd_param_count() == N.NPARAM
     assert lib.ryd_summary_width() == N.NSUMMARY
     assert lib.ryd_state_width(0, 3) == 25 and lib.ryd_state_width(1, 3) == 18
