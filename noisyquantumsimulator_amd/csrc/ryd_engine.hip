@@ -712,6 +712,291 @@ __global__ __launch_bounds__(BLOCK) void ket_cheb_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Noise-free kets by exact block propagators (the default ket method)
+// ---------------------------------------------------------------------------
+// H conserves which atoms sit in |0>, so each computational input stays in a block:
+// |00> (energy 0: amplitude 1), {|01>, |0r>} (2 x 2; |10> is its atom-swap mirror)
+// and {|11>, |1r>, |r1>, |rr>}, where |11> only reaches the exchange-symmetric
+// {|11>, |+> = (|1r> + |r1>)/sqrt2, |rr>} (3 x 3).  With Omega = a e^{i phi}:
+//   H2 = D2 Hr2 D2^dag, Hr2 = [[d1, a/2], [a/2, -Delta]],                 D2 = diag(1, e^{i phi})
+//   H3 = D3 Hr3 D3^dag, Hr3 = [[2 d1, a/sqrt2, 0], [a/sqrt2, d1 - Delta, a/sqrt2],
+//                              [0, a/sqrt2, V - 2 Delta]],                 D3 = diag(1, e^{i phi}, e^{2 i phi})
+// (energies e = {0, d1, -Delta} per atom + V on |rr>, couplings Omega/2 as apply_K).
+// exp(-i Hr2 dt) in closed form; exp(-i Hr3 dt) = Q diag(e^{-i lambda dt}) Q^T from a
+// cyclic Jacobi eigendecomposition of the real symmetric Hr3 (backward stable: the
+// result is exp(-i (H + E) dt) with |E| ~ eps |H|, the same class of error as the
+// Chebyshev series).  Segments that differ only in laser phase share the real factors
+// (the phase frame), so LP square and smooth JP build once per point, bang-bang once
+// per segment; a segment then costs 13 complex MACs + the frame phases.  One lane per
+// point (ket_cheb_kernel, the cross-check method, spends ~x Chebyshev terms of an
+// 84-FMA generator on each of 4 lanes per segment, x = |H| dt up to ~5e3 on LP).
+struct KetBlocks {
+  double a, dl, dt;                          // the real factors below are for these
+  double u2[3][2];                           // exp(-i Hr2 dt): m00, m01 (= m10), m11 (re, im)
+  double u3[6][2];                           // exp(-i Hr3 dt): 00 01 02 11 12 22 (complex symmetric)
+};
+
+__device__ __forceinline__ void jacobi_rot(double (&A)[3][3], double (&Q)[3][3], int p, int q) {
+  const double apq = A[p][q];
+  if (apq == 0.0) return;
+  const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+  const double t = copysign(1.0, theta) / (fabs(theta) + sqrt(fma(theta, theta, 1.0)));   // inf theta -> 0
+  const double c = 1.0 / sqrt(fma(t, t, 1.0)), sn = t * c;
+  A[p][p] = fma(-t, apq, A[p][p]);
+  A[q][q] = fma(t, apq, A[q][q]);
+  A[p][q] = A[q][p] = 0.0;
+  const int r = 3 - p - q;
+  const double arp = A[r][p], arq = A[r][q];
+  A[r][p] = A[p][r] = fma(c, arp, -sn * arq);
+  A[r][q] = A[q][r] = fma(sn, arp, c * arq);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double qkp = Q[k][p], qkq = Q[k][q];
+    Q[k][p] = fma(c, qkp, -sn * qkq);
+    Q[k][q] = fma(sn, qkp, c * qkq);
+  }
+}
+
+__device__ __forceinline__ void ket_blocks_build(KetBlocks& B, double a, double dl, double dt, double d1,
+                                                 double V) {
+  B.a = a;
+  B.dl = dl;
+  B.dt = dt;
+  // 2 x 2: exp(-i (c I + M) dt) = e^{-i c dt} (cos(r dt) I - i sin(r dt)/r M), M = [[h, w], [w, -h]]
+  {
+    const double c = 0.5 * (d1 - dl), h = 0.5 * (d1 + dl), w = 0.5 * a;
+    const double r = sqrt(fma(h, h, w * w));
+    double sr, cr, sc, cc;
+    sincos(r * dt, &sr, &cr);
+    sincos(c * dt, &sc, &cc);
+    const double snc = r > 0.0 ? sr / r : dt;
+    // e^{-i c dt} = cc - i sc times (cr - i snc h, -i snc w, cr + i snc h)
+    const double m[3][2] = {{cr, -snc * h}, {0.0, -snc * w}, {cr, snc * h}};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      B.u2[k][0] = fma(cc, m[k][0], sc * m[k][1]);
+      B.u2[k][1] = fma(cc, m[k][1], -sc * m[k][0]);
+    }
+  }
+  // 3 x 3 symmetric block: Jacobi (fixed 6 sweeps: quadratic convergence, exact zeros stop)
+  {
+    const double g = a * 0.70710678118654752440;     // a / sqrt2
+    double A[3][3] = {{2.0 * d1, g, 0.0}, {g, d1 - dl, g}, {0.0, g, V - 2.0 * dl}};
+    double Q[3][3] = {{1.0, 0.0, 0.0}, {0.0, 1.0, 0.0}, {0.0, 0.0, 1.0}};
+#pragma unroll 1
+    for (int sweep = 0; sweep < 6; ++sweep) {
+      jacobi_rot(A, Q, 0, 1);
+      jacobi_rot(A, Q, 0, 2);
+      jacobi_rot(A, Q, 1, 2);
+    }
+    double er[3], ei[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double sn, cs;
+      sincos(A[k][k] * dt, &sn, &cs);
+      er[k] = cs;
+      ei[k] = -sn;
+    }
+    const int I[6] = {0, 0, 0, 1, 1, 2}, J[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+      double re = 0.0, im = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double w = Q[I[e]][k] * Q[J[e]][k];
+        re = fma(w, er[k], re);
+        im = fma(w, ei[k], im);
+      }
+      B.u3[e][0] = re;
+      B.u3[e][1] = im;
+    }
+  }
+}
+
+// the segment in polar form: amplitude a >= 0, laser phase (c, sn), detuning, duration
+template <int PROTO>
+__device__ __forceinline__ void ket_seg_polar(const PointP& q, int s, int n_steps, int shape, double& a, double& c,
+                                              double& sn, double& dl, double& dt) {
+  const Seg g = segment<PROTO>(q, s, n_steps, shape);
+  dl = g.dl;
+  dt = g.dt;
+  if (PROTO == RYD_PROTO_SMOOTH_JP || PROTO == RYD_PROTO_BANGBANG) {
+    a = q.Om;                                  // |Omega e^{i phi}| = Omega (the reference's H)
+    c = q.Om > 0.0 ? g.om_re / q.Om : 1.0;
+    sn = q.Om > 0.0 ? g.om_im / q.Om : 0.0;
+    if (PROTO == RYD_PROTO_BANGBANG && s >= q.nseg) a = 0.0;
+  } else if (PROTO == RYD_PROTO_LP_SQUARE && s == 1) {
+    // H2 = H(Omega xi): |xi| = 1 (compute_phase_shift_xi) to rounding -> the same real
+    // factors as segment 0 (one build, as the Lindblad kernel's frame_ok); other xi as given
+    const double m = sqrt(fma(q.xr, q.xr, q.xi * q.xi));
+    const bool unit = fabs(m - 1.0) <= 1e-14;
+    a = unit ? q.Om : q.Om * m;
+    c = unit ? q.xr : (m > 0.0 ? q.xr / m : 1.0);
+    sn = unit ? q.xi : (m > 0.0 ? q.xi / m : 0.0);
+  } else {
+    a = sqrt(fma(g.om_re, g.om_re, g.om_im * g.om_im));
+    if (g.om_im == 0.0 && g.om_re >= 0.0) a = g.om_re;   // phase-0 segments: exact amplitude
+    c = a > 0.0 ? g.om_re / a : 1.0;
+    sn = a > 0.0 ? g.om_im / a : 0.0;
+  }
+}
+
+#define CMUL_RE(ar, ai, br, bi) fma(ar, br, -(ai) * (bi))
+#define CMUL_IM(ar, ai, br, bi) fma(ar, bi, (ai) * (br))
+
+template <int PROTO, int KD>
+__global__ __launch_bounds__(BLOCK) void ket_block_kernel(
+    const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ st, int64_t lds,
+    double* __restrict__ sm, int64_t ldm, uint32_t* __restrict__ status, int n_steps, int shape) {
+  const int64_t gi = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (gi >= n) return;
+  const int64_t i = gi;
+  const PointP q = load_point<PROTO>(prm, ldp, i);
+  const bool valid = point_valid<PROTO>(q, n_steps);
+  // |01> block (c01, c0r) and the |11> symmetric block (c11, c+, crr), complex
+  double b2r[2] = {1.0, 0.0}, b2i[2] = {0.0, 0.0};
+  double b3r[3] = {1.0, 0.0, 0.0}, b3i[3] = {0.0, 0.0, 0.0};
+  KetBlocks K;
+  K.a = K.dl = K.dt = -1.0;                  // nothing built yet
+  bool over_cap = false;
+  int nseg_used = 0, nbuild = 0;
+  const int nseg = n_segments<PROTO>(n_steps);
+  for (int s = 0; s < nseg && valid; ++s) {
+    double a, c, sn, dl, dt;
+    ket_seg_polar<PROTO>(q, s, n_steps, shape, a, c, sn, dl, dt);
+    if (!(dt > 0.0)) continue;               // empty / padding segment: identity
+    {                                        // the ket_cheb_kernel's step cap, same bound
+      Seg g;
+      g.om_re = a;
+      g.om_im = 0.0;
+      g.dl = dl;
+      g.dt = dt;
+      double emin, emax;
+      h_bounds(g, q.V, q.d1, emin, emax);
+      if (!(0.5 * (emax - emin) * dt <= X_CAP)) {
+        over_cap = true;
+        continue;
+      }
+    }
+    if (!(a == K.a && dl == K.dl && dt == K.dt)) {
+      ket_blocks_build(K, a, dl, dt, q.d1, q.V);
+      ++nbuild;
+    }
+    ++nseg_used;
+    // frame: w = D^dag b, w <- U w, b = D w  (D = diag(1, e^{i phi}[, e^{2 i phi}]))
+    const double c2 = fma(c, c, -sn * sn), s2 = 2.0 * c * sn;
+    {
+      const double xr = CMUL_RE(b2r[1], b2i[1], c, -sn), xi = CMUL_IM(b2r[1], b2i[1], c, -sn);
+      const double yr = CMUL_RE(K.u2[0][0], K.u2[0][1], b2r[0], b2i[0]) +
+                        CMUL_RE(K.u2[1][0], K.u2[1][1], xr, xi);
+      const double yi = CMUL_IM(K.u2[0][0], K.u2[0][1], b2r[0], b2i[0]) +
+                        CMUL_IM(K.u2[1][0], K.u2[1][1], xr, xi);
+      const double zr = CMUL_RE(K.u2[1][0], K.u2[1][1], b2r[0], b2i[0]) +
+                        CMUL_RE(K.u2[2][0], K.u2[2][1], xr, xi);
+      const double zi = CMUL_IM(K.u2[1][0], K.u2[1][1], b2r[0], b2i[0]) +
+                        CMUL_IM(K.u2[2][0], K.u2[2][1], xr, xi);
+      b2r[0] = yr;
+      b2i[0] = yi;
+      b2r[1] = CMUL_RE(zr, zi, c, sn);
+      b2i[1] = CMUL_IM(zr, zi, c, sn);
+    }
+    {
+      const double wr[3] = {b3r[0], CMUL_RE(b3r[1], b3i[1], c, -sn), CMUL_RE(b3r[2], b3i[2], c2, -s2)};
+      const double wi[3] = {b3i[0], CMUL_IM(b3r[1], b3i[1], c, -sn), CMUL_IM(b3r[2], b3i[2], c2, -s2)};
+      const int U[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+      double yr[3], yi[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        double accr = 0.0, acci = 0.0;
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+          const double ur = K.u3[U[r][m]][0], ui = K.u3[U[r][m]][1];
+          accr = fma(ur, wr[m], fma(-ui, wi[m], accr));
+          acci = fma(ur, wi[m], fma(ui, wr[m], acci));
+        }
+        yr[r] = accr;
+        yi[r] = acci;
+      }
+      b3r[0] = yr[0];
+      b3i[0] = yi[0];
+      b3r[1] = CMUL_RE(yr[1], yi[1], c, sn);
+      b3i[1] = CMUL_IM(yr[1], yi[1], c, sn);
+      b3r[2] = CMUL_RE(yr[2], yi[2], c2, s2);
+      b3i[2] = CMUL_IM(yr[2], yi[2], c2, s2);
+    }
+  }
+  // rows of the ket layout (2 D doubles per input, D = KD^2, basis KD*a1 + a2; |r-> rows
+  // of dim 4 stay zero): input x = 4 i + k
+  constexpr int D = KD * KD;
+  const double h = 0.70710678118654752440;
+  // (input k, basis b) -> amplitude; every other entry is an exact zero
+  const double c1r = h * b3r[1], c1i = h * b3i[1];
+#pragma unroll
+  for (int b = 0; b < D; ++b) {
+    const int a1 = b / KD, a2 = b % KD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double re = 0.0, im = 0.0;
+      if (k == 0 && b == 0) re = 1.0;                                        // |00>
+      if (k == 1 && a1 == 0 && a2 == 1) { re = b2r[0]; im = b2i[0]; }        // |01> -> c01 |01>
+      if (k == 1 && a1 == 0 && a2 == 2) { re = b2r[1]; im = b2i[1]; }        //        + c0r |0r>
+      if (k == 2 && a1 == 1 && a2 == 0) { re = b2r[0]; im = b2i[0]; }        // |10>: atom-swap mirror
+      if (k == 2 && a1 == 2 && a2 == 0) { re = b2r[1]; im = b2i[1]; }
+      if (k == 3 && a1 == 1 && a2 == 1) { re = b3r[0]; im = b3i[0]; }        // |11> -> c11 |11>
+      if (k == 3 && ((a1 == 1 && a2 == 2) || (a1 == 2 && a2 == 1))) { re = c1r; im = c1i; }   // c+ |+>
+      if (k == 3 && a1 == 2 && a2 == 2) { re = b3r[2]; im = b3i[2]; }        //  + crr |rr>
+      st[(int64_t)(2 * b) * lds + 4 * i + k] = re;
+      st[(int64_t)(2 * b + 1) * lds + 4 * i + k] = im;
+    }
+  }
+  uint32_t stat = valid ? 0u : RYD_STATUS_BAD_INPUT;
+  if (over_cap) stat |= RYD_STATUS_STEP_CAP;
+  bool fin = true;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) fin = fin && isfinite(b2r[e]) && isfinite(b2i[e]);
+#pragma unroll
+  for (int e = 0; e < 3; ++e) fin = fin && isfinite(b3r[e]) && isfinite(b3i[e]);
+  if (!fin) stat |= RYD_STATUS_NONFINITE;
+  // compute_CZ_fidelity pure branch (RG/simulation.py:483-631), as ket_cheb_kernel
+  const double orr[4] = {1.0, b2r[0], b2r[0], b3r[0]}, oii[4] = {0.0, b2i[0], b2i[0], b3i[0]};
+  double p[4], ph[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    p[x] = orr[x] * orr[x] + oii[x] * oii[x];
+    ph[x] = atan2(oii[x], orr[x]);
+  }
+  double cp = ph[3] - ph[1] - ph[2] + ph[0];
+  cp = cp + M_PI;
+  cp = cp - 2.0 * M_PI * floor(cp / (2.0 * M_PI));
+  cp = cp - M_PI;
+  const double err = fmin(fabs(cp - M_PI), fabs(cp + M_PI));
+  const double cerr = cos(err / 2);
+  const double pen = cerr * cerr;
+  const double avgp = 0.25 * (p[0] + p[1] + p[2] + p[3]);
+  const double avgf = 0.25 * (p[0] + p[1] + p[2] + p[3] * pen);
+  double nrm11 = 0.0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) nrm11 += b3r[e] * b3r[e] + b3i[e] * b3i[e];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    sm[(int64_t)(RYD_S_POP0 + x) * ldm + i] = p[x];
+    sm[(int64_t)(RYD_S_OV_RE0 + x) * ldm + i] = orr[x];
+    sm[(int64_t)(RYD_S_OV_IM0 + x) * ldm + i] = oii[x];
+  }
+  sm[(int64_t)RYD_S_AVG_POP * ldm + i] = avgp;
+  sm[(int64_t)RYD_S_CTRL_PHASE * ldm + i] = cp;
+  sm[(int64_t)RYD_S_PENALTY * ldm + i] = pen;
+  sm[(int64_t)RYD_S_AVG_F * ldm + i] = avgf;
+  sm[(int64_t)RYD_S_NMV_USEFUL * ldm + i] = (double)nseg_used;     // block segment applications
+  sm[(int64_t)RYD_S_NMV_EXEC * ldm + i] = (double)nseg_used;
+  sm[(int64_t)RYD_S_TRACE11 * ldm + i] = nrm11;
+  sm[(int64_t)RYD_S_NSQUARE * ldm + i] = (double)nbuild;           // propagator builds
+  status[i] = stat;
+}
+#undef CMUL_RE
+#undef CMUL_IM
+
+// ---------------------------------------------------------------------------
 // dim 4 (mJ sublevels |r+>, |r->) Lindblad kernel on the 36-dim real sector
 // ---------------------------------------------------------------------------
 // RG/hamiltonians.py:655-663 (sigma+ drives |1> <-> |r+> only), :741-753 (-Delta on
@@ -1944,12 +2229,13 @@ __device__ __forceinline__ void apply_coh(const Gen& A0, const Gen& B0, const CG
 }
 
 template <int PROTO, int KIND>
-__global__ __launch_bounds__(BLOCK) void coherence_cheb_kernel(
-    const double* __restrict__ prm, int64_t n, int64_t ldp, double* __restrict__ out, int64_t ldo,
-    uint32_t* __restrict__ status, int n_steps, int shape) {
+__device__ __forceinline__ void coherence_sector(const double* __restrict__ prm, int64_t n, int64_t ldp,
+                                                 double* __restrict__ out, int64_t ldo,
+                                                 uint32_t* __restrict__ status, int n_steps, int shape,
+                                                 int64_t blk) {
   constexpr int NIN = KIND < 2 ? 2 : 1;     // inputs of this sector per point
   constexpr int NV = KIND < 2 ? 20 : 8;
-  const int64_t gid = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t gid = blk * BLOCK + threadIdx.x;
   const bool live = gid < NIN * n;
   const int64_t i = live ? gid / NIN : (n - 1);
   const int sub = (int)(gid % NIN);
@@ -2009,6 +2295,23 @@ __global__ __launch_bounds__(BLOCK) void coherence_cheb_kernel(
   (void)nexec;
 }
 
+// All four coherence sectors in ONE launch: blocks [0, b0) sector 0, [b0, b1) sector 1,
+// [b1, b2) sector 2, then sector 3 (block-uniform branch).  The sectors used to be four
+// back-to-back launches of 2n, 2n, n and n lanes -- each far below one wave per SIMD at
+// C2 sizes, so the device idled through four serial latency-bound tails; together they
+// fill the chip once (the two 20-double sectors, whose lanes run longest, first).
+template <int PROTO>
+__global__ __launch_bounds__(BLOCK) void coherence_cheb_kernel(const double* __restrict__ prm, int64_t n,
+                                                               int64_t ldp, double* __restrict__ out, int64_t ldo,
+                                                               uint32_t* __restrict__ status, int n_steps,
+                                                               int shape, int64_t b0, int64_t b1, int64_t b2) {
+  const int64_t b = blockIdx.x;
+  if (b < b0) coherence_sector<PROTO, 0>(prm, n, ldp, out, ldo, status, n_steps, shape, b);
+  else if (b < b1) coherence_sector<PROTO, 1>(prm, n, ldp, out, ldo, status, n_steps, shape, b - b0);
+  else if (b < b2) coherence_sector<PROTO, 2>(prm, n, ldp, out, ldo, status, n_steps, shape, b - b1);
+  else coherence_sector<PROTO, 3>(prm, n, ldp, out, ldo, status, n_steps, shape, b - b2);
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -2054,6 +2357,15 @@ bool use_sym16(const ryd_batch_desc* d) {
           d->protocol == RYD_PROTO_SMOOTH_JP);
 }
 
+// Kets under the default (auto) method: the exact block-propagator kernel, one lane per
+// point; RYD_METHOD_CHEB_VECTOR keeps the 4-lane Chebyshev state-vector kernel (the
+// cross-check), as does RYD_KET_BLOCK=0.
+bool use_ket_block(const ryd_batch_desc* d) {
+  const char* e = getenv("RYD_KET_BLOCK");
+  if (e && e[0] == '0') return false;
+  return d->evolution == RYD_EVOL_KET && d->method == RYD_METHOD_CHEBYSHEV;
+}
+
 KernelFn pick_kernel(const ryd_batch_desc* d) {
   const bool sym = (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0;
   if (d->dim == 4) {
@@ -2067,6 +2379,13 @@ KernelFn pick_kernel(const ryd_batch_desc* d) {
           return sym ? lindblad4_cheb_kernel<RYD_PROTO_BANGBANG, true> : lindblad4_cheb_kernel<RYD_PROTO_BANGBANG, false>;
         case RYD_PROTO_SMOOTH_JP:
           return sym ? lindblad4_cheb_kernel<RYD_PROTO_SMOOTH_JP, true> : lindblad4_cheb_kernel<RYD_PROTO_SMOOTH_JP, false>;
+      }
+    } else if (use_ket_block(d)) {
+      switch (d->protocol) {
+        case RYD_PROTO_LP_SQUARE: return ket_block_kernel<RYD_PROTO_LP_SQUARE, 4>;
+        case RYD_PROTO_LP_SHAPED: return ket_block_kernel<RYD_PROTO_LP_SHAPED, 4>;
+        case RYD_PROTO_BANGBANG: return ket_block_kernel<RYD_PROTO_BANGBANG, 4>;
+        case RYD_PROTO_SMOOTH_JP: return ket_block_kernel<RYD_PROTO_SMOOTH_JP, 4>;
       }
     } else {
       switch (d->protocol) {
@@ -2097,6 +2416,13 @@ KernelFn pick_kernel(const ryd_batch_desc* d) {
         return sym ? lindblad_cheb_kernel<RYD_PROTO_BANGBANG, true> : lindblad_cheb_kernel<RYD_PROTO_BANGBANG, false>;
       case RYD_PROTO_SMOOTH_JP:
         return sym ? lindblad_cheb_kernel<RYD_PROTO_SMOOTH_JP, true> : lindblad_cheb_kernel<RYD_PROTO_SMOOTH_JP, false>;
+    }
+  } else if (d->evolution == RYD_EVOL_KET && use_ket_block(d)) {
+    switch (d->protocol) {
+      case RYD_PROTO_LP_SQUARE: return ket_block_kernel<RYD_PROTO_LP_SQUARE, 3>;
+      case RYD_PROTO_LP_SHAPED: return ket_block_kernel<RYD_PROTO_LP_SHAPED, 3>;
+      case RYD_PROTO_BANGBANG: return ket_block_kernel<RYD_PROTO_BANGBANG, 3>;
+      case RYD_PROTO_SMOOTH_JP: return ket_block_kernel<RYD_PROTO_SMOOTH_JP, 3>;
     }
   } else if (d->evolution == RYD_EVOL_KET) {
     switch (d->protocol) {
@@ -2238,7 +2564,8 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
     return launch_jp_split(d, dp, n, ldp, ds, lds, dm, ldm, dstat, stream);
   KernelFn k = pick_kernel(d);
   if (!k) return fail(RYD_ERR_UNSUPPORTED, "no kernel for this descriptor");
-  const int64_t blocks = use_propagator(d) ? (n + PPB - 1) / PPB : (4 * n + BLOCK - 1) / BLOCK;
+  const int64_t blocks = use_propagator(d) ? (n + PPB - 1) / PPB
+                        : use_ket_block(d) ? (n + BLOCK - 1) / BLOCK : (4 * n + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
   int ns = d->n_steps, sh = d->shape;
   void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
@@ -2250,22 +2577,18 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
 template <int PROTO>
 int launch_coherences_proto(const double* dp, int64_t n, int64_t ldp, double* dc, int64_t ldc,
                             uint32_t* dstat, int ns, int sh, hipStream_t stream) {
-  using CFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, uint32_t*, int, int);
-  const CFn fns[4] = {coherence_cheb_kernel<PROTO, 0>, coherence_cheb_kernel<PROTO, 1>,
-                      coherence_cheb_kernel<PROTO, 2>, coherence_cheb_kernel<PROTO, 3>};
-  for (int k = 0; k < 4; ++k) {
-    const int64_t lanes = (k < 2 ? 2 : 1) * n;
-    const int64_t blocks = (lanes + BLOCK - 1) / BLOCK;
-    if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
-    void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&dc, (void*)&ldc,
-                    (void*)&dstat, (void*)&ns, (void*)&sh};
-    HIPCHK(hipLaunchKernel((const void*)fns[k], dim3((unsigned)blocks), dim3(BLOCK), args, 0, stream));
-  }
+  const int64_t nb2 = (2 * n + BLOCK - 1) / BLOCK, nb1 = (n + BLOCK - 1) / BLOCK;
+  const int64_t b0 = nb2, b1 = 2 * nb2, b2 = 2 * nb2 + nb1, blocks = 2 * nb2 + 2 * nb1;
+  if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
+  void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&dc, (void*)&ldc, (void*)&dstat,
+                  (void*)&ns, (void*)&sh, (void*)&b0, (void*)&b1, (void*)&b2};
+  HIPCHK(hipLaunchKernel((const void*)coherence_cheb_kernel<PROTO>, dim3((unsigned)blocks), dim3(BLOCK), args, 0,
+                         stream));
   return RYD_OK;
 }
 
-// The four coherence-sector launches of one batch; status is cleared first and
-// each kernel ORs its bits in.
+// The coherence sectors of one batch (one launch); status is cleared first and each
+// sector ORs its bits in.
 int launch_coherences(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, double* dc,
                       int64_t ldc, uint32_t* dstat, hipStream_t stream) {
   if (n == 0) return RYD_OK;

@@ -256,8 +256,11 @@ class Engine:
         desc = make_desc(protocol, evolution, n_steps, shape, symmetric_atoms(params), method,
                          dim=dim, rtol=rtol, atol=atol, max_steps=max_steps)
         w = N.STATE_WIDTH_DIM[dim][evolution]
-        state = np.zeros((w, 4 * n), dtype=np.float64)
-        summ = np.zeros((N.NSUMMARY, n), dtype=np.float64)
+        # every kernel writes every state row and summary column of every point, so the
+        # outputs need no zero fill (np.zeros of the 8 MB C2 state costs ~0.3 ms of page
+        # zeroing per call; tools/unpack_probe.py)
+        state = np.empty((w, 4 * n), dtype=np.float64)
+        summ = np.empty((N.NSUMMARY, n), dtype=np.float64)
         status = np.zeros(n, dtype=np.uint32)
         st = N.Stats()
         dptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
@@ -363,6 +366,63 @@ class DeviceBatch:
         N.check(lib.ryd_memcpy_d2h(h, s, status.ctypes.data, self.d_status, status.nbytes))
         return EngineResult(self.evolution, self.n, state, summ, status, 0.0, 0.0, 0.0,
                             summ[N.S["NMV_USEFUL"]].sum(), summ[N.S["NMV_EXEC"]].sum(), self.dim)
+
+    def free(self):
+        for p in self._bufs:
+            self.eng.lib.ryd_free(self.eng.handle, self.slot, p)
+        self._bufs = []
+
+
+class CoherenceDeviceBatch:
+    """Process-map coherence sectors (ryd_run_coherences_device: the four
+    coherence_cheb_kernel launches) with inputs resident in HBM, for timed re-runs."""
+
+    def __init__(self, engine: Engine, params: np.ndarray, protocol: str, n_steps: Optional[int] = None,
+                 shape: str = "square", slot: int = 0):
+        self.eng, self.slot = engine, slot
+        lib = engine.lib
+        params = np.ascontiguousarray(params, dtype=np.float64)
+        self.n = n = params.shape[1]
+        if n_steps is None:
+            n_steps = default_n_steps(protocol, params)
+        self.desc = make_desc(protocol, "lindblad", n_steps, shape, symmetric_atoms(params), "cheb_vector")
+        self._bufs = []
+
+        def alloc(nbytes):
+            p = ctypes.c_void_p()
+            N.check(lib.ryd_malloc(engine.handle, slot, nbytes, ctypes.byref(p)))
+            self._bufs.append(p)
+            return p
+        self.d_params = alloc(params.nbytes)
+        self.d_coh = alloc(8 * N.NCOH * n)
+        self.d_status = alloc(4 * n)
+        N.check(lib.ryd_memcpy_h2d(engine.handle, slot, self.d_params, params.ctypes.data, params.nbytes))
+
+    def launch(self, timed: bool = False) -> float:
+        ms = ctypes.c_float(0.0)
+        N.check(self.eng.lib.ryd_run_coherences_device(
+            self.eng.handle, self.slot, ctypes.byref(self.desc), self.d_params, self.n, self.n,
+            self.d_coh, self.n, self.d_status, None, ctypes.byref(ms) if timed else None))
+        return float(ms.value)
+
+    def mark(self, which: int):
+        N.check(self.eng.lib.ryd_mark(self.eng.handle, self.slot, which))
+
+    def mark_elapsed(self) -> float:
+        ms = ctypes.c_float(0.0)
+        N.check(self.eng.lib.ryd_mark_elapsed(self.eng.handle, self.slot, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def synchronize(self):
+        N.check(self.eng.lib.ryd_synchronize(self.eng.handle))
+
+    def fetch(self) -> Tuple[np.ndarray, np.ndarray]:
+        lib, h, s = self.eng.lib, self.eng.handle, self.slot
+        coh = np.zeros((N.NCOH, self.n))
+        status = np.zeros(self.n, dtype=np.uint32)
+        N.check(lib.ryd_memcpy_d2h(h, s, coh.ctypes.data, self.d_coh, coh.nbytes))
+        N.check(lib.ryd_memcpy_d2h(h, s, status.ctypes.data, self.d_status, status.nbytes))
+        return coh, status
 
     def free(self):
         for p in self._bufs:

@@ -39,21 +39,24 @@ def _apparatus_kwargs(**over):
 
 def omega_delta_grid(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.0),
                      delta_over_omega=(0.30, 0.45), omega_tau: float = 4.29268,
-                     include_noise: bool = True, delta_slice: Optional[slice] = None) -> PH.DerivedBatch:
+                     include_noise: bool = True, delta_slice: Optional[slice] = None,
+                     pulse_shape: str = "square", hilbert_space_dim: int = 3) -> PH.DerivedBatch:
     """C2: (Omega, Delta) sweep of the LP square CZ gate on the medium apparatus.
 
     Omega/2pi = linspace(1, 10) MHz is produced the physical way, by scaling the
     480 nm leg power (Omega ∝ sqrt(P2)); Delta/Omega = linspace(0.30, 0.45);
     Omega*tau = 4.29268; V = C6/R^6 = 2pi x 1233.83 MHz; every noise rate from the
-    reference formulas per point."""
+    reference formulas per point.  ``pulse_shape`` / ``hilbert_space_dim``
+    give the same grid for the shaped-LP and dim-4 kernels (bench.py secondary lines)."""
     si, n, kw = omega_delta_call(n_omega, n_delta, omega_mhz, delta_over_omega, omega_tau, include_noise,
-                                 delta_slice)
+                                 delta_slice, pulse_shape, hilbert_space_dim)
     return PH.derive_batch(si, n=n, **kw)
 
 
 def omega_delta_call(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.0),
                      delta_over_omega=(0.30, 0.45), omega_tau: float = 4.29268,
-                     include_noise: bool = True, delta_slice: Optional[slice] = None):
+                     include_noise: bool = True, delta_slice: Optional[slice] = None,
+                     pulse_shape: str = "square", hilbert_space_dim: int = 3):
     """The C2 grid as (simulation_inputs, n, keyword arguments) of derive_batch /
     simulate_CZ_gate_batch (the end-to-end form of omega_delta_grid)."""
     warnings.simplefilter("ignore")
@@ -67,8 +70,9 @@ def omega_delta_call(n_omega: int = 100, n_delta: int = 100, omega_mhz=(1.0, 10.
         dom = dom[delta_slice]
     OM, DOM = np.meshgrid(om, dom, indexing="ij")
     p2 = MEDIUM["laser_2_power"] * (OM.ravel() / om0) ** 2
-    si = CF.LPSimulationInputs(excitation=exc, omega_tau=omega_tau)
+    si = CF.LPSimulationInputs(excitation=exc, omega_tau=omega_tau, pulse_shape=pulse_shape)
     return si, p2.size, dict(**_apparatus_kwargs(), include_noise=include_noise,
+                             hilbert_space_dim=hilbert_space_dim,
                              overrides=dict(laser_2_power=p2, delta_over_omega=DOM.ravel()))
 
 
