@@ -242,6 +242,13 @@ def end_to_end_c2():
 FLOP_PER_LADDER_STEP = 8 * 124 + 2 * 54
 FLOP_PER_BLOCK_SQUARING = 8 * (8 + 64 + 512) + 2 * 84
 FLOP_PER_TRAJ_REDUCTION = 378 * 14
+# the exchange-symmetry-adapted kernel (traj3s_kernel, the default): a ladder step is the
+# quadratic form x^dag G_l x over the 12 block instances (86 complex-pair terms: 344
+# flops); an accepted step applies (I + X_l) (66 complex MACs + the norm: 636 flops); one
+# ladder level is 71 complex MACs + 46 adds (squaring) + 71 complex MACs (its Gram level)
+FLOP_PER_SYM_STEP = 344
+FLOP_PER_SYM_APPLY = 8 * 66 + 2 * 54
+FLOP_PER_SYM_LEVEL = 8 * 71 + 92 + 8 * 71
 C5_BYTES_PER_POINT = 8 * 15 + 8 * (1458 + 729 + 10) + 4   # params read; rho, se, summary, status
 
 
@@ -283,11 +290,17 @@ def run_c5(args, ws, rank, local, pg):
     assert np.all(res.status == 0), "engine reported per-point failures"
     it_use = float(res.col("ITER_USEFUL").sum())
     it_exec = float(res.col("ITER_EXEC").sum())
-    flops = (it_use * FLOP_PER_LADDER_STEP + float(res.col("NSQUARE").sum()) * FLOP_PER_BLOCK_SQUARING
-             + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
+    napply = float(res.col("RESERVED").sum())
+    if napply > 0:                                  # traj3s_kernel (adapted basis)
+        flops = (it_use * FLOP_PER_SYM_STEP + napply * FLOP_PER_SYM_APPLY
+                 + float(res.col("NSQUARE").sum()) * FLOP_PER_SYM_LEVEL + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
+    else:                                           # traj3_kernel (RYD_T_SYM=0)
+        flops = (it_use * FLOP_PER_LADDER_STEP + float(res.col("NSQUARE").sum()) * FLOP_PER_BLOCK_SQUARING
+                 + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     achieved_gbs = C5_BYTES_PER_POINT * n / (k_ms * 1e-3) / 1e9
-    tr = _measured_traffic("c5", "mcwf", n, "traj3_kernel") if args.n_traj == 256 else None
+    tr = (_measured_traffic("c5", "mcwf", n, "traj3s_kernel" if napply > 0 else "traj3_kernel")
+          if args.n_traj == 256 else None)
     traffic = tr["bytes_per_launch"] if tr else None
     total = SW.C5_POINTS * args.steps
     out = {
@@ -303,7 +316,8 @@ def run_c5(args, ws, rank, local, pg):
                    "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS",
                    "ladder_levels": db.desc.ladder_levels, "placement": _placement(ws, local, dev)},
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": "traj3_kernel", "kernel_ms": k_ms, "kernel_ms_isolated": k_iso,
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": "traj3s_kernel" if napply > 0 else "traj3_kernel",
+                     "kernel_ms": k_ms, "kernel_ms_isolated": k_iso,
                      "flops_per_launch": flops, "exec_over_useful": it_exec / max(it_use, 1.0),
                      "mean_jumps": float(res.col("MEAN_JUMPS").mean())},
         "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -189,7 +189,7 @@ extern "C" {
 #define RYD_TS_ITER_EXEC   6     /* lane-steps the waves executed (divergence included) */
 #define RYD_TS_NLADDER     7     /* ladders built (one per distinct |Omega|, Delta, dt) */
 #define RYD_TS_NSQUARE     8     /* block squarings performed building them             */
-#define RYD_TS_RESERVED    9
+#define RYD_TS_RESERVED    9     /* adapted-basis kernel: (I + X) applications; else 0 */
 #define RYD_T_NSUMMARY     10
 
 typedef struct ryd_traj_desc {

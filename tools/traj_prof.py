@@ -1,0 +1,39 @@
+"""Per-wave phase totals of traj3_kernel from the RYD_T_PROF build variant
+(build/libryd_tprof.so: shader-clock phase sums written over the C5 summary columns).
+Usage on the GPU box:
+    RYD_ENGINE_LIB=$PWD/build/libryd_tprof.so python tools/traj_prof.py [ladder]
+"""
+import sys
+import warnings
+
+import numpy as np
+
+from noisyquantumsimulator_amd import engine as E
+from noisyquantumsimulator_amd import sweeps as SW
+from noisyquantumsimulator_amd import trajectories as TR
+
+warnings.simplefilter("ignore")
+L = int(sys.argv[1]) if len(sys.argv) > 1 else TR.DEFAULT_LADDER
+eng = E.Engine()
+params = E.pack_params(SW.blockade_grid_3atom())
+db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=256, ladder_levels=L,
+                              seed=20260215, point_offset=0)
+for _ in range(2):
+    db.launch()
+db.synchronize()
+ms = db.launch(timed=True)
+r = db.fetch()
+names = ["ladder+no-jump", "classify", "walk", "reduce", "outputs"]
+cols = ["MEAN_JUMPS", "FRAC_JUMPED", "MAX_JUMPS", "TRACE", "QUBIT_POP"]
+tot = r.col("RESERVED")
+print(f"C5 L={L}: kernel {ms:.3f} ms, {params.shape[1]} waves; per-wave cycles (mean over waves):")
+for nm, c in zip(names, cols):
+    v = r.col(c)
+    print(f"  {nm:15s} mean {v.mean():10.0f}  ({100 * v.mean() / tot.mean():5.1f} %)  p90 {np.percentile(v, 90):10.0f}")
+print(f"  {'total':15s} mean {tot.mean():10.0f}  max {tot.max():10.0f}")
+use, ex = r.col("ITER_USEFUL"), r.col("ITER_EXEC")
+print(f"  ladder steps useful {use.sum():.3g}, executed {ex.sum():.3g} (exec/useful {ex.sum() / use.sum():.2f}); "
+      f"walk cycles per executed wave-step {r.col('MAX_JUMPS').sum() / (ex.sum() / 64):.0f}")
+if r.col("NSQUARE").max() < 100:      # the sym kernel's prof build: ladder phase split
+    print(f"  ladder build split (pass 1): taylor {r.col('ITER_USEFUL').mean():.0f}  squarings "
+          f"{r.col('ITER_EXEC').mean():.0f}  levels {r.col('NLADDER').mean():.0f}  s0 {r.col('NSQUARE').mean():.2f}")
