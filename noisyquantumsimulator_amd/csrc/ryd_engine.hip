@@ -55,8 +55,6 @@ struct ryd_slot_work {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool ev_ok = false;
   hipEvent_t mark[2] = {nullptr, nullptr};   // ryd_mark / ryd_mark_elapsed
-  void* tbuf = nullptr;     // trajectory scratch rows (traj3q_kernel), grown on demand
-  size_t tcap = 0;
 };
 
 // one stream per device slot; defined at global scope (the header's opaque type)
@@ -2784,38 +2782,9 @@ int ensure_slot_work(ryd_handle* h, int k, size_t bytes) {
   return RYD_OK;
 }
 
-bool tq_enabled();
-bool t_sym_enabled();
-size_t tq_scratch_bytes(int64_t n);
-
-// The quad trajectory kernel's scratch rows for slot k (device already set), or NULL when
-// the protocol keeps traj3s_kernel.  Grows on demand; hipFree waits for earlier launches.
-int traj_scratch(ryd_handle* h, int k, const ryd_traj_desc* d, int64_t n, double** out) {
-  *out = nullptr;
-  if (n <= 0 || !tq_enabled() || !t_sym_enabled() ||
-      !(d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_SMOOTH_JP))
-    return RYD_OK;
-  if ((int)h->work.size() < (int)h->dev.size()) h->work.resize(h->dev.size());
-  ryd_slot_work& w = h->work[k];
-  const size_t bytes = tq_scratch_bytes(n);
-  if (w.tcap < bytes) {
-    if (w.tbuf) HIPCHK(hipFree(w.tbuf));
-    w.tbuf = nullptr;
-    w.tcap = 0;
-    if (hipMalloc(&w.tbuf, bytes) != hipSuccess) {
-      w.tbuf = nullptr;
-      return fail(RYD_ERR_ALLOC, "trajectory scratch allocation failed");
-    }
-    w.tcap = bytes;
-  }
-  *out = (double*)w.tbuf;
-  return RYD_OK;
-}
-
 void release_slot_work(ryd_slot_work& w) {
   if (w.dbuf) (void)hipFree(w.dbuf);
   if (w.hbuf) (void)hipHostFree(w.hbuf);
-  if (w.tbuf) (void)hipFree(w.tbuf);
   for (int j = 0; j < 4; ++j)
     if (w.ev[j]) (void)hipEventDestroy(w.ev[j]);
   for (int j = 0; j < 2; ++j)
@@ -3246,13 +3215,8 @@ int ryd_run_trajectories(ryd_handle* h, const ryd_traj_desc* desc, const double*
       h, params, n, ld_params, outs, out_status,
       [&](const double* dp, int64_t cnt, int64_t ldp, int64_t off, const std::vector<double*>& o,
           uint32_t* dst, hipStream_t s) {
-        int k = 0;
-        while (k + 1 < (int)h->stream.size() && h->stream[k] != s) ++k;
-        double* scr = nullptr;
-        const int e = traj_scratch(h, k, desc, cnt, &scr);
-        if (e) return e;
         return launch_traj(desc, dp, cnt, ldp, off, o[0], RYD_T_RHO_WIDTH, o[1], RYD_T_SE_WIDTH, o[2], cnt,
-                           out_records ? o[3] : nullptr, dst, scr, s);
+                           out_records ? o[3] : nullptr, dst, s);
       },
       kms, hms, dms);
   if (rc) return rc;
@@ -3290,11 +3254,8 @@ int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* de
     rc = timer.start(s);
     if (rc) return rc;
   }
-  double* scr = nullptr;
-  rc = traj_scratch(h, slot, desc, n, &scr);
-  if (rc) return rc;
   rc = launch_traj(desc, d_params, n, ld_params, point_offset, d_rho, ld_rho, d_se, ld_se, d_summary, ld_summary,
-                   d_records, d_status, scr, s);
+                   d_records, d_status, s);
   if (rc) return rc;
   return elapsed_ms ? timer.stop(s, elapsed_ms) : RYD_OK;
 }
