@@ -276,6 +276,12 @@ FLOP_PER_TRAJ_REDUCTION = 378 * 14
 FLOP_PER_SYM_STEP = 344
 FLOP_PER_SYM_APPLY = 8 * 66 + 2 * 54
 FLOP_PER_SYM_LEVEL = 8 * 71 + 92 + 8 * 71
+# the exact-jump-time kernel (traj3e_kernel, ladder_levels = 0): one evaluation of psi(t) is
+# 12 complex exponentials (counted as their 2 scaling multiplies, not as flops of their own),
+# 26 complex scalings, the 66-MAC block product and the norm + decay sums (27 x 4); a
+# change to eigen-coordinates (segment start, after each jump) is another 66 complex MACs
+FLOP_PER_EIG_EVAL = 2 * 12 + 6 * 26 + 8 * 66 + 4 * 27
+FLOP_PER_EIG_COEFFS = 8 * 66
 C5_BYTES_PER_POINT = 8 * 15 + 8 * (1458 + 729 + 10) + 4   # params read; rho, se, summary, status
 
 
@@ -292,7 +298,7 @@ def run_c5(args, ws, rank, local, pg):
     dev = _rank_device(local)
     eng = E.Engine(devices=[dev])
     db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=args.n_traj,
-                                  ladder_levels=args.ladder if args.ladder > 0 else TR.DEFAULT_LADDER,
+                                  ladder_levels=args.ladder if args.ladder >= 0 else TR.DEFAULT_LADDER,
                                   seed=20260215, point_offset=off)
     for _ in range(args.warmup):
         db.launch()
@@ -318,7 +324,13 @@ def run_c5(args, ws, rank, local, pg):
     it_use = float(res.col("ITER_USEFUL").sum())
     it_exec = float(res.col("ITER_EXEC").sum())
     napply = float(res.col("RESERVED").sum())
-    if napply > 0:                                  # traj3s_kernel (adapted basis)
+    exact = db.desc.ladder_levels == TR.N.T["EXACT"]
+    kernel = "traj3e_kernel" if exact else ("traj3s_kernel" if napply > 0 else "traj3_kernel")
+    if exact:                                       # traj3e_kernel: evaluations + basis changes
+        ntr = args.n_traj
+        ncoef = float((res.col("MEAN_JUMPS") * ntr + 2.0 * res.col("FRAC_JUMPED") * ntr + 2.0).sum())
+        flops = it_use * FLOP_PER_EIG_EVAL + ncoef * FLOP_PER_EIG_COEFFS + n * ntr * FLOP_PER_TRAJ_REDUCTION
+    elif napply > 0:                                # traj3s_kernel (adapted basis)
         flops = (it_use * FLOP_PER_SYM_STEP + napply * FLOP_PER_SYM_APPLY
                  + float(res.col("NSQUARE").sum()) * FLOP_PER_SYM_LEVEL + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
     else:                                           # traj3_kernel (RYD_T_SYM=0)
@@ -326,7 +338,7 @@ def run_c5(args, ws, rank, local, pg):
                  + n * args.n_traj * FLOP_PER_TRAJ_REDUCTION)
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     achieved_gbs = C5_BYTES_PER_POINT * n / (k_ms * 1e-3) / 1e9
-    tr = (_measured_traffic("c5", "mcwf", n, "traj3s_kernel" if napply > 0 else "traj3_kernel")
+    tr = (_measured_traffic("c5", "mcwf", n, kernel)
           if args.n_traj == 256 else None)
     traffic = tr["bytes_per_launch"] if tr else None
     total = SW.C5_POINTS * args.steps
@@ -340,10 +352,11 @@ def run_c5(args, ws, rank, local, pg):
                                 "per point (Philox4x32-10), |+++> input, medium-apparatus rates"),
                    "points_per_gpu": n, "global_points": SW.C5_POINTS, "trajectories_per_point": args.n_traj,
                    "trajectories_per_s": total * args.n_traj / dt_max,
-                   "parallelism": f"range-shard x{ws}", "method": "MCWF, binary expm1 ladder in LDS",
+                   "parallelism": f"range-shard x{ws}", "method": ("MCWF, exact jump times (Newton on the eigen-decomposed H_eff)" if exact
+                              else "MCWF, binary expm1 ladder in LDS"),
                    "ladder_levels": db.desc.ladder_levels, "placement": _placement(ws, local, dev)},
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": "traj3s_kernel" if napply > 0 else "traj3_kernel",
+                     "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kernel,
                      "kernel_ms": k_ms, "kernel_ms_isolated": k_iso,
                      "flops_per_launch": flops, "exec_over_useful": it_exec / max(it_use, 1.0),
                      "mean_jumps": float(res.col("MEAN_JUMPS").mean())},
@@ -561,7 +574,8 @@ def main():
     ap.add_argument("--workload", default="c2",
                     choices=["c2", "c3", "c4", "c5", *AUX, *OPT_PUBLISHED])
     ap.add_argument("--n-traj", type=int, default=256, help="C5 trajectories per point")
-    ap.add_argument("--ladder", type=int, default=0, help="C5 ladder levels (0: trajectories.DEFAULT_LADDER)")
+    ap.add_argument("--ladder", type=int, default=-1,
+                    help="C5 ladder levels (0: exact jump times; -1: trajectories.DEFAULT_LADDER)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test: no GPU
     args = ap.parse_args()
 

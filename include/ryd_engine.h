@@ -174,6 +174,7 @@ extern "C" {
 #define RYD_T_DIM          27
 #define RYD_T_RHO_WIDTH    1458
 #define RYD_T_SE_WIDTH     729
+#define RYD_T_EXACT        0     /* ladder_levels: exact jump times (eigen-decomposed H_eff) */
 #define RYD_T_LADDER_MAX   40    /* jump times resolved to segment / 2^ladder_levels     */
 #define RYD_T_REC_WIDTH    64
 #define RYD_T_REC_NJUMPS   54
@@ -198,7 +199,10 @@ typedef struct ryd_traj_desc {
   int32_t shape;           /* RYD_SHAPE_* (LP_SHAPED) */
   int32_t n_steps;         /* as ryd_batch_desc */
   int32_t n_traj;          /* trajectories per point: a multiple of 64 */
-  int32_t ladder_levels;   /* 1 .. RYD_T_LADDER_MAX (16 recommended) */
+  int32_t ladder_levels;   /* RYD_T_EXACT: exact jump times (Newton on the eigen-
+                              decomposed H_eff, the default); 1 ..
+                              RYD_T_LADDER_MAX: the ladder walk, jump times resolved
+                              to segment / 2^ladder_levels */
   uint64_t seed;
   double psi0[2 * RYD_T_DIM];  /* normalised initial ket, (re, im) interleaved */
 } ryd_traj_desc;

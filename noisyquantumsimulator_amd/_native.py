@@ -44,7 +44,7 @@ C = dict(K0=0, K1=8, K2=16, K3=18)
 NCOH = 20
 
 # three-atom quantum-jump trajectories (ryd_run_trajectories)
-T = dict(DIM=27, RHO_WIDTH=1458, SE_WIDTH=729, LADDER_MAX=40, REC_WIDTH=64, REC_NJUMPS=54,
+T = dict(DIM=27, RHO_WIDTH=1458, SE_WIDTH=729, EXACT=0, LADDER_MAX=40, REC_WIDTH=64, REC_NJUMPS=54,
          REC_JUMP0=55, REC_JUMPS=4, REC_ITERS=63)
 TS = dict(MEAN_JUMPS=0, FRAC_JUMPED=1, MAX_JUMPS=2, TRACE=3, QUBIT_POP=4, ITER_USEFUL=5,
           ITER_EXEC=6, NLADDER=7, NSQUARE=8, RESERVED=9)

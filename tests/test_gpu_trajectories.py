@@ -149,6 +149,30 @@ def test_trajectories_match_exact_time_oracle(eng):
     assert checked > 5
 
 
+@pytest.mark.parametrize("idx,scale", [(1200, 40.0), (77, 60.0), (4095, 40.0)])
+def test_exact_jump_times_match_oracle(eng, idx, scale):
+    """ladder_levels = RYD_T_EXACT: every jump time is the root the oracle's brentq finds
+    (Newton on the eigen-decomposed H_eff), not the end of a ladder quantum -- so later
+    jumps agree as tightly as the first, and so do the final kets."""
+    p = _c5([idx], scale=scale)
+    psi0 = TR.plus_state()
+    r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=256, seed=77, ladder_levels=N.T["EXACT"],
+                            records=True)
+    assert r.status[0] == 0
+    nj, tj, cj, kets = r.n_jumps()[0], r.jump_times()[0], r.jump_channels()[0], r.kets()[0]
+    dt = p[N.P["TAU"], 0]
+    checked = 0
+    for t in range(32):
+        k, jumps = O3.mc_trajectory(p[:, 0], "lp_square", psi0, point=0, traj=t, seed=77)
+        assert nj[t] == len(jumps), t
+        for m, (tt, ch) in enumerate(jumps[:N.T["REC_JUMPS"]]):
+            assert cj[t, m] == ch
+            assert abs(tj[t, m] - tt) <= 1e-10 * dt, (t, m, tj[t, m], tt)
+            checked += 1
+        assert abs(np.vdot(k, kets[t])) > 1 - 1e-12, t
+    assert checked > 5
+
+
 def test_launch_shape_and_partition_independence(eng):
     p = _c5(list(range(0, 4096, 512)), scale=20.0)
     a = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5, records=True)
@@ -178,7 +202,7 @@ def test_bad_inputs(eng):
     with pytest.raises(N.EngineError):
         TR.run_trajectories(eng, p, "lp_square", n_traj=100)
     with pytest.raises(N.EngineError):
-        TR.run_trajectories(eng, p, "lp_square", n_traj=256, ladder_levels=0)
+        TR.run_trajectories(eng, p, "lp_square", n_traj=256, ladder_levels=-1)
 
 
 def test_c5_full_grid_properties(eng):

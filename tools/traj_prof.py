@@ -34,6 +34,6 @@ print(f"  {'total':15s} mean {tot.mean():10.0f}  max {tot.max():10.0f}")
 use, ex = r.col("ITER_USEFUL"), r.col("ITER_EXEC")
 print(f"  ladder steps useful {use.sum():.3g}, executed {ex.sum():.3g} (exec/useful {ex.sum() / use.sum():.2f}); "
       f"walk cycles per executed wave-step {r.col('MAX_JUMPS').sum() / (ex.sum() / 64):.0f}")
-if r.col("NSQUARE").max() < 100:      # the sym kernel's prof build: ladder phase split
+if L != 0 and r.col("NSQUARE").max() < 100:   # the sym kernel's prof build: ladder phase split
     print(f"  ladder build split (pass 1): taylor {r.col('ITER_USEFUL').mean():.0f}  squarings "
           f"{r.col('ITER_EXEC').mean():.0f}  levels {r.col('NLADDER').mean():.0f}  s0 {r.col('NSQUARE').mean():.2f}")
