@@ -200,9 +200,10 @@ typedef struct ryd_traj_desc {
   int32_t n_steps;         /* as ryd_batch_desc */
   int32_t n_traj;          /* trajectories per point: a multiple of 64 */
   int32_t ladder_levels;   /* RYD_T_EXACT: exact jump times (Newton on the eigen-
-                              decomposed H_eff, the default); 1 ..
-                              RYD_T_LADDER_MAX: the ladder walk, jump times resolved
-                              to segment / 2^ladder_levels */
+                              decomposed H_eff), for schedules with a
+                              constant |Omega| and Delta (not a shaped LP envelope);
+                              1 .. RYD_T_LADDER_MAX: the ladder walk, jump times
+                              resolved to segment / 2^ladder_levels */
   uint64_t seed;
   double psi0[2 * RYD_T_DIM];  /* normalised initial ket, (re, im) interleaved */
 } ryd_traj_desc;

@@ -32,12 +32,24 @@ DIM = 27
 LABELS3 = tuple(f"{a}{b}{c}" for a in "01" for b in "01" for c in "01")
 QUBIT_INDEX3 = tuple(9 * a + 3 * b + c for a in (0, 1) for b in (0, 1) for c in (0, 1))
 CHANNELS = ("|1><r|", "|0><r|", "P_r", "P_1")       # channel code = 4 * atom + c
-# Jump times are resolved to segment / 2^L and a jump lands at the end of its quantum.
-# For the C5 LP-square points Omega * tau = 4.29, so the delay shifts the conditional
-# state by ~Omega * tau / 2^(L+1) = 3e-5 per jump at L = 16 (P(jump) ~ 0.1: ~4e-6 in
-# rho), against a standard error of ~1e-2 at 256 trajectories; L = 24 (1e-7) costs
-# ~25 % more ladder steps for no visible change.
-DEFAULT_LADDER = 16
+# Jump times.  ladder_levels = N.T["EXACT"] (0): the root of ||psi(t)||^2 = r, by Newton on
+# the eigen-decomposed H_eff (traj3e_kernel) -- the oracle's own definition, and the
+# fastest C5 kernel; it needs |Omega| and Delta constant over a point's
+# segments.  ladder_levels = L >= 1: the binary ladder walk (traj3s_kernel), jump times
+# resolved to segment / 2^L; at L = 16 the delay shifts the conditional state by
+# ~Omega tau / 2^(L+1) = 3e-5 per jump on the C5 points, against a standard error of
+# ~1e-2 at 256 trajectories.  DEFAULT_LADDER (None) picks exact times wherever they
+# apply and the L = 16 ladder for a shaped LP envelope.
+DEFAULT_LADDER = None
+LADDER_WALK = 16
+
+
+def resolve_ladder(ladder_levels: Optional[int], protocol: str, shape: str = "square") -> int:
+    """The ladder_levels a descriptor gets: ``None`` -> exact jump times, or the L = 16
+    ladder where exact mode does not apply (a shaped LP envelope)."""
+    if ladder_levels is not None:
+        return int(ladder_levels)
+    return LADDER_WALK if (protocol == "lp_shaped" and shape != "square") else N.T["EXACT"]
 
 
 def basis_index(a0: int, a1: int, a2: int) -> int:
@@ -74,7 +86,7 @@ def _psi_array(psi0: np.ndarray) -> np.ndarray:
 
 
 def make_traj_desc(protocol: str, psi0: np.ndarray, n_traj: int = 256, seed: int = 0,
-                   ladder_levels: int = DEFAULT_LADDER, n_steps: int = 0,
+                   ladder_levels: Optional[int] = DEFAULT_LADDER, n_steps: int = 0,
                    shape: str = "square") -> N.TrajDesc:
     d = N.TrajDesc()
     d.abi_version = N.RYD_ABI_VERSION
@@ -82,7 +94,7 @@ def make_traj_desc(protocol: str, psi0: np.ndarray, n_traj: int = 256, seed: int
     d.shape = N.SHAPE[shape]
     d.n_steps = n_steps
     d.n_traj = n_traj
-    d.ladder_levels = ladder_levels
+    d.ladder_levels = resolve_ladder(ladder_levels, protocol, shape)
     d.seed = seed & 0xFFFFFFFFFFFFFFFF
     d.psi0[:] = list(_psi_array(psi0))
     return d
@@ -137,7 +149,7 @@ class TrajectoryResult:
 
 
 def run_trajectories(engine: Engine, params: np.ndarray, protocol: str, psi0: Optional[np.ndarray] = None,
-                     n_traj: int = 256, seed: int = 0, ladder_levels: int = DEFAULT_LADDER,
+                     n_traj: int = 256, seed: int = 0, ladder_levels: Optional[int] = DEFAULT_LADDER,
                      n_steps: Optional[int] = None, shape: str = "square",
                      records: bool = False) -> TrajectoryResult:
     """Host-buffer form: every point of ``params`` (``pack_params`` columns; atom-A
@@ -170,7 +182,7 @@ class TrajectoryDeviceBatch:
     range shards launched with their global ``point_offset``."""
 
     def __init__(self, engine: Engine, params: np.ndarray, protocol: str, psi0: Optional[np.ndarray] = None,
-                 n_traj: int = 256, seed: int = 0, ladder_levels: int = DEFAULT_LADDER,
+                 n_traj: int = 256, seed: int = 0, ladder_levels: Optional[int] = DEFAULT_LADDER,
                  n_steps: Optional[int] = None, shape: str = "square", slot: int = 0,
                  point_offset: int = 0, records: bool = False):
         self.eng, self.slot, self.point_offset = engine, slot, point_offset

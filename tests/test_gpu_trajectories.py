@@ -46,9 +46,15 @@ def _two_atom(si, n=2):
     return E.pack_params(b)
 
 
+LADDERS = [16, N.T["EXACT"]]          # the ladder walk and the exact-jump-time kernel
+
+
+@pytest.mark.parametrize("ladder", LADDERS)
 @pytest.mark.parametrize("protocol,n_steps,shape", [("lp_square", None, "square"), ("bangbang", None, "square"),
                                                     ("smooth_jp", 60, "square"), ("lp_shaped", 40, "cosine")])
-def test_zero_rates_equal_pure_evolution(eng, protocol, n_steps, shape):
+def test_zero_rates_equal_pure_evolution(eng, protocol, n_steps, shape, ladder):
+    if ladder == N.T["EXACT"] and protocol == "lp_shaped":
+        pytest.skip("a shaped envelope has no constant H_eff: exact mode refuses it (test_bad_inputs)")
     if protocol == "lp_square":
         p = _c5([0, 700, 2100, 4095])
     elif protocol == "bangbang":
@@ -60,7 +66,7 @@ def test_zero_rates_equal_pure_evolution(eng, protocol, n_steps, shape):
     p[4:12] = 0.0
     ns = n_steps if n_steps is not None else E.default_n_steps(protocol, p)
     psi0 = TR.plus_state()
-    r = TR.run_trajectories(eng, p, protocol, psi0, n_traj=256, n_steps=ns, shape=shape)
+    r = TR.run_trajectories(eng, p, protocol, psi0, n_traj=256, n_steps=ns, shape=shape, ladder_levels=ladder)
     assert np.all(r.status == 0)
     assert np.all(r.col("MEAN_JUMPS") == 0)
     for i in range(p.shape[1]):
@@ -81,11 +87,12 @@ def test_spectator_atom_matches_two_atom_engine(eng):
         np.testing.assert_allclose(r.rho[i], np.outer(psi, psi.conj()), atol=1e-10, rtol=0)
 
 
-def test_noisy_mean_rho_within_standard_error(eng):
+@pytest.mark.parametrize("ladder", LADDERS)
+def test_noisy_mean_rho_within_standard_error(eng, ladder):
     idx = [5, 1800, 4000]
     p = _c5(idx, scale=30.0)
     psi0 = TR.plus_state()
-    r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=2048, seed=20260215)
+    r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=2048, seed=20260215, ladder_levels=ladder)
     assert np.all(r.status == 0)
     assert np.all(r.col("MEAN_JUMPS") > 0.05)
     np.testing.assert_allclose(r.col("TRACE"), 1.0, atol=1e-12)
@@ -102,15 +109,17 @@ def test_noisy_mean_rho_within_standard_error(eng):
     assert 0.3 < np.mean(z2) < 2.0, z2                        # the errors ARE standard errors
 
 
+@pytest.mark.parametrize("ladder", LADDERS)
 @pytest.mark.parametrize("protocol,n_steps", [("bangbang", None), ("smooth_jp", 12)])
-def test_noisy_multi_segment_protocols(eng, protocol, n_steps):
+def test_noisy_multi_segment_protocols(eng, protocol, n_steps, ladder):
     """Bang-bang rebuilds the ladder every segment (different lengths) inside the
     jumper rounds; smooth JP rotates the frame every segment."""
     p = _two_atom(CF.JPSimulationInputs if protocol == "bangbang" else CF.SmoothJPSimulationInputs, n=1)
     p[4:12] *= 5.0                                            # ~1-2 jumps per trajectory
     ns = n_steps if n_steps is not None else E.default_n_steps(protocol, p)
     psi0 = TR.plus_state()
-    r = TR.run_trajectories(eng, p, protocol, psi0, n_traj=2048, seed=99, n_steps=ns, records=True)
+    r = TR.run_trajectories(eng, p, protocol, psi0, n_traj=2048, seed=99, n_steps=ns, records=True,
+                            ladder_levels=ladder)
     assert r.status[0] == 0 and r.col("MEAN_JUMPS")[0] > 0.05
     ref = O3.exact_rho(p[:, 0], protocol, psi0, n_steps=ns)
     d = np.abs(r.rho[0] - ref)
@@ -173,42 +182,51 @@ def test_exact_jump_times_match_oracle(eng, idx, scale):
     assert checked > 5
 
 
-def test_launch_shape_and_partition_independence(eng):
+@pytest.mark.parametrize("ladder", LADDERS)
+def test_launch_shape_and_partition_independence(eng, ladder):
     p = _c5(list(range(0, 4096, 512)), scale=20.0)
-    a = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5, records=True)
-    b = TR.run_trajectories(eng, p, "lp_square", n_traj=512, seed=5, records=True)
+    kw = dict(ladder_levels=ladder)
+    a = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5, records=True, **kw)
+    b = TR.run_trajectories(eng, p, "lp_square", n_traj=512, seed=5, records=True, **kw)
     np.testing.assert_array_equal(a.records, b.records[:, :256])     # a trajectory = its stream
-    c = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5)
+    c = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5, **kw)
     np.testing.assert_array_equal(a.rho, c.rho)                         # deterministic
-    # two device-side range shards with their global offsets == one batch
+    # device-side range shards with their global offsets == one batch (the exact kernel
+    # groups several points per wave: odd shard boundaries regroup them)
     outs = []
-    for lo, hi in ((0, 3), (3, 8)):
-        db = TR.TrajectoryDeviceBatch(eng, p[:, lo:hi], "lp_square", n_traj=256, seed=5, point_offset=lo)
+    for lo, hi in ((0, 3), (3, 4), (4, 8)):
+        db = TR.TrajectoryDeviceBatch(eng, p[:, lo:hi], "lp_square", n_traj=256, seed=5, point_offset=lo, **kw)
         db.launch()
         db.synchronize()
         outs.append(db.fetch())
         db.free()
     np.testing.assert_array_equal(np.concatenate([o.rho for o in outs]), a.rho)
-    d = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=6)
+    d = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=6, **kw)
     assert not np.array_equal(d.rho, a.rho)
 
 
-def test_bad_inputs(eng):
+@pytest.mark.parametrize("ladder", LADDERS)
+def test_bad_inputs(eng, ladder):
     p = _c5([1, 2, 3])
     p[N.P["OMEGA"], 1] = 0.0
-    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256)
+    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256, ladder_levels=ladder)
     assert r.status[1] & N.STATUS_BAD_INPUT and r.status[0] == 0 and r.status[2] == 0
     assert np.all(r.rho[1] == 0)
     with pytest.raises(N.EngineError):
         TR.run_trajectories(eng, p, "lp_square", n_traj=100)
     with pytest.raises(N.EngineError):
         TR.run_trajectories(eng, p, "lp_square", n_traj=256, ladder_levels=-1)
+    with pytest.raises(N.EngineError):                      # exact mode needs a constant H_eff
+        TR.run_trajectories(eng, _two_atom(lambda excitation: CF.LPSimulationInputs(
+            excitation=excitation, pulse_shape="cosine")), "lp_shaped", n_traj=256, n_steps=40, shape="cosine",
+            ladder_levels=N.T["EXACT"])
 
 
-def test_c5_full_grid_properties(eng):
+@pytest.mark.parametrize("ladder", LADDERS)
+def test_c5_full_grid_properties(eng, ladder):
     warnings.simplefilter("ignore")
     p = E.pack_params(SW.blockade_grid_3atom())
-    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=20260215)
+    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=20260215, ladder_levels=ladder)
     assert r.n == 4096 and np.all(r.status == 0)
     np.testing.assert_allclose(r.col("TRACE"), 1.0, atol=1e-12)
     np.testing.assert_allclose(r.rho, np.conj(np.transpose(r.rho, (0, 2, 1))), atol=0)

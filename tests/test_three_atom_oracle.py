@@ -117,7 +117,11 @@ def test_traj_desc_layout_and_states():
     assert ctypes.sizeof(N.TrajDesc) == 464
     d = TR.make_traj_desc("lp_square", TR.plus_state(), 512, seed=3)
     v = np.array(d.psi0[:])
-    assert abs((v ** 2).sum() - 1) < 1e-15 and d.n_traj == 512 and d.ladder_levels == TR.DEFAULT_LADDER
+    assert abs((v ** 2).sum() - 1) < 1e-15 and d.n_traj == 512 and d.ladder_levels == N.T["EXACT"]
+    # exact jump times by default; the ladder walk where they do not apply (shaped envelope)
+    assert TR.make_traj_desc("lp_shaped", TR.plus_state(), 256, shape="cosine").ladder_levels == TR.LADDER_WALK
+    assert TR.make_traj_desc("lp_shaped", TR.plus_state(), 256, shape="square").ladder_levels == N.T["EXACT"]
+    assert TR.make_traj_desc("bangbang", TR.plus_state(), 256, ladder_levels=20).ladder_levels == 20
     assert TR.basis_index(1, 1, 1) == 13 and TR.QUBIT_INDEX3 == (0, 1, 3, 4, 9, 10, 12, 13)
     flat = np.arange(1458, dtype=float)[None]
     rho = TR.unpack_rho(flat)

@@ -13,7 +13,7 @@ from noisyquantumsimulator_amd import sweeps as SW
 from noisyquantumsimulator_amd import trajectories as TR
 
 warnings.simplefilter("ignore")
-L = int(sys.argv[1]) if len(sys.argv) > 1 else TR.DEFAULT_LADDER
+L = int(sys.argv[1]) if len(sys.argv) > 1 else TR.resolve_ladder(TR.DEFAULT_LADDER, "lp_square")
 eng = E.Engine()
 params = E.pack_params(SW.blockade_grid_3atom())
 db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=256, ladder_levels=L,
