@@ -127,10 +127,15 @@ def test_noisy_multi_segment_protocols(eng, protocol, n_steps, ladder):
     assert np.all((d < 1e-9) | (d < 5.5 * se + 1e-8)), (d / se).max()
     # and one-to-one against the exact-jump-time oracle for a few trajectories
     nj, cj, kets = r.n_jumps()[0], r.jump_channels()[0], r.kets()[0]
+    exact = ladder == N.T["EXACT"]
+    tj = r.jump_times()[0]
+    t_total = sum(dt for _, _, dt in O3.schedule(p[:, 0], protocol, ns))
     for t in range(6):
         k, jumps = O3.mc_trajectory(p[:, 0], protocol, psi0, point=0, traj=t, seed=99, n_steps=ns)
         assert nj[t] == len(jumps) and all(cj[t, m] == ch for m, (_, ch) in enumerate(jumps[:4]))
-        assert abs(np.vdot(k, kets[t])) > 1 - 1e-6
+        assert abs(np.vdot(k, kets[t])) > 1 - (1e-12 if exact else 1e-6)
+        if exact:     # every segment boundary and phase frame crossed at the oracle's jump times
+            assert all(abs(tj[t, m] - tt) <= 1e-10 * t_total for m, (tt, _) in enumerate(jumps[:4]))
 
 
 def test_trajectories_match_exact_time_oracle(eng):
