@@ -1,6 +1,6 @@
 """Benchmark: Lindblad parameter points/s on the C2 sweep (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N --steps K --warmup W] [--workload c2|c3|c4|c5|shaped|dim4|ket|coherence|opt_lp|opt_smooth]
+    python bench.py [--gpus N --steps K --warmup W] [--workload c1|c2|c3|c4|c5|shaped|dim4|ket|coherence|opt_lp|opt_smooth]
 
 A step = one propagation of this rank's 10,000-point LP-square (Omega, Delta)
 sweep -- every point's 4 basis density matrices through both pulses, noise
@@ -285,6 +285,85 @@ FLOP_PER_EIG_COEFFS = 8 * 66
 C5_BYTES_PER_POINT = 8 * 15 + 8 * (1458 + 729 + 10) + 4   # params read; rho, se, summary, status
 
 
+def run_c1(args, ws, rank, local, pg):
+    """C1: ONE dim-3 LP-square point with one collapse operator, as a
+    single-point latency -- what every unmodified per-point caller of the reference
+    (examples/research_parameter_sweeps.py:119, RG/optimize_cz_gate.py:1117,
+    RG/optimization.py:531) sees per simulate_CZ_gate call.  Reported: the engine path on
+    the exact C1 inputs (host-buffer ryd_run_batch + the reference phase epilogue), the
+    drop-in simulate_CZ_gate on the reference's default noisy LP configuration (derive +
+    engine + epilogue + SimulationResult), each the median of warm calls, and the oracle's
+    ZVODE CPU path on the C1 point beside them."""
+    from noisyquantumsimulator_amd import configurations as CF
+    from noisyquantumsimulator_amd import engine as E
+    from noisyquantumsimulator_amd import simulation as SIM
+    from noisyquantumsimulator_amd import sweeps as SW
+    dev = _rank_device(local)
+    eng = E.Engine(devices=[dev])
+    prm = SW.c1_params()
+    reps = max(args.steps, 20)
+
+    def engine_call():
+        t0 = time.perf_counter()
+        r = eng.run(prm, "lp_square", "lindblad")
+        t1 = time.perf_counter()
+        ph, fl = E.mixed_phase(r.state, 1, 3, gauge_check=True)
+        cp, pen = SIM._cp_penalty(ph)
+        pops = r.populations()[0]
+        avg = float((pops[0] + pops[1] + pops[2] + pops[3] * pen[0]) / 4.0)
+        return (t1 - t0) * 1e3, (time.perf_counter() - t1) * 1e3, r.kernel_ms, avg, int(r.status[0] | fl[0])
+    for _ in range(max(args.warmup, 3)):
+        engine_call()
+    runs = [engine_call() for _ in range(reps)]
+    eng_ms = [x[0] for x in runs]
+    epi_ms = [x[1] for x in runs]
+    k_ms = [x[2] for x in runs]
+    tot = [x[0] + x[1] for x in runs]
+    avg_f, st = runs[-1][3], runs[-1][4]
+    # the drop-in per-point call on the reference's default noisy LP configuration
+    si = CF.LPSimulationInputs()
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for _ in range(3):
+            SIM.simulate_CZ_gate(si, include_noise=True)
+        dt = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            res = SIM.simulate_CZ_gate(si, include_noise=True)
+            dt.append((time.perf_counter() - t0) * 1e3)
+        parts = []
+        for _ in range(reps):
+            br = SIM.simulate_CZ_gate_batch(si, 1, include_noise=True, return_states=True)
+            parts.append(br.timings)
+    med = lambda v: float(np.median(v))
+    dropin = {k: med([p[k] for p in parts]) for k in ("derive_ms", "engine_ms", "epilogue_ms", "total_ms")}
+    dropin["simulate_CZ_gate_ms"] = med(dt)
+    dropin["result_assembly_ms"] = med(dt) - dropin["total_ms"]
+    dropin["avg_fidelity"] = float(res.avg_fidelity)
+    out = {
+        "metric": "C1 single-point latency (one 2-atom 3-level Rydberg CZ point, 1 collapse op)",
+        "value": med(tot), "unit": "ms", "n_gpus": 1, "steps": reps, "warmup": max(args.warmup, 3),
+        "ms_per_step": med(tot), "higher_is_better": False, "scaling": "none", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "C1: dim 3, LP square, Omega = 2 pi 5 MHz, V/Omega = 100, Delta/Omega = 0.377371, "
+                               "Omega tau = 4.29268, xi from compute_phase_shift_xi, one c_op sqrt(1/140 us) |1><r| (x) I",
+                   "placement": _placement(1, local, dev)},
+        "engine_path": {"engine_call_ms": med(eng_ms), "kernel_ms": med(k_ms), "epilogue_ms": med(epi_ms),
+                        "avg_fidelity": avg_f, "status": st,
+                        "note": "host-buffer ryd_run_batch (pack, H2D, kernel, D2H) + ryd_mixed_phase with the "
+                                "16-probe gauge check"},
+        "dropin_default_lp": dict(dropin, note="simulate_CZ_gate(LPSimulationInputs(), include_noise=True): the "
+                                               "reference's default noisy LP point (14 c_ops collapsed to 8 channels); "
+                                               "breakdown from simulate_CZ_gate_batch(n=1) timings"),
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(10, 1, "c1")
+        out["cpu_over_gpu"] = out["cpu_baseline"]["value"] / out["value"]
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
 def run_c5(args, ws, rank, local, pg):
     """C5: 4096-point (Omega, V/Omega) three-atom blockade grid, 256 quantum-jump
     trajectories per point, strong-scaled over the ranks (range shards keyed by their
@@ -292,7 +371,10 @@ def run_c5(args, ws, rank, local, pg):
     from noisyquantumsimulator_amd import engine as E
     from noisyquantumsimulator_amd import sweeps as SW
     from noisyquantumsimulator_amd import trajectories as TR
-    batch, off = SW.c5_rank_shard(rank, ws)
+    if args.c5_shards:           # one GPU, one rank's shard of an N-way split (the scaling proxy)
+        batch, off = SW.c5_rank_shard(args.c5_rank, args.c5_shards, order=args.c5_order)
+    else:
+        batch, off = SW.c5_rank_shard(rank, ws, order=args.c5_order)
     params = E.pack_params(batch)
     n = batch.n
     dev = _rank_device(local)
@@ -325,7 +407,9 @@ def run_c5(args, ws, rank, local, pg):
     it_exec = float(res.col("ITER_EXEC").sum())
     napply = float(res.col("RESERVED").sum())
     exact = db.desc.ladder_levels == TR.N.T["EXACT"]
-    kernel = "traj3e_kernel" if exact else ("traj3s_kernel" if napply > 0 else "traj3_kernel")
+    wg = os.environ.get("RYD_T_WG", "1") != "0"
+    kernel = (("traj3w_kernel" if wg else "traj3e_kernel") if exact
+              else ("traj3s_kernel" if napply > 0 else "traj3_kernel"))
     if exact:                                       # traj3e_kernel: evaluations + basis changes
         ntr = args.n_traj
         ncoef = float((res.col("MEAN_JUMPS") * ntr + 2.0 * res.col("FRAC_JUMPED") * ntr + 2.0).sum())
@@ -341,7 +425,7 @@ def run_c5(args, ws, rank, local, pg):
     tr = (_measured_traffic("c5", "mcwf", n, kernel)
           if args.n_traj == 256 else None)
     traffic = tr["bytes_per_launch"] if tr else None
-    total = SW.C5_POINTS * args.steps
+    total = (n if args.c5_shards else SW.C5_POINTS) * args.steps
     out = {
         "metric": "Lindblad param-points/sec (2-atom Rydberg CZ sweep); achieved HBM GB/s vs peak",
         "value": total / dt_max, "unit": "points/s", "n_gpus": ws, "steps": args.steps,
@@ -351,6 +435,8 @@ def run_c5(args, ws, rank, local, pg):
                                 f"blockade grid, LP square, {args.n_traj} quantum-jump trajectories "
                                 "per point (Philox4x32-10), |+++> input, medium-apparatus rates"),
                    "points_per_gpu": n, "global_points": SW.C5_POINTS, "trajectories_per_point": args.n_traj,
+                   "shard": (f"rank {args.c5_rank} of {args.c5_shards} (1-GPU scaling proxy)" if args.c5_shards
+                             else None),
                    "trajectories_per_s": total * args.n_traj / dt_max,
                    "parallelism": f"range-shard x{ws}", "method": ("MCWF, exact jump times (Newton on the eigen-decomposed H_eff)" if exact
                               else "MCWF, binary expm1 ladder in LDS"),
@@ -572,8 +658,13 @@ def main():
     ap.add_argument("--method", default="chebyshev",
                     choices=["chebyshev", "cheb_squaring", "cheb_vector"])
     ap.add_argument("--workload", default="c2",
-                    choices=["c2", "c3", "c4", "c5", *AUX, *OPT_PUBLISHED])
+                    choices=["c1", "c2", "c3", "c4", "c5", *AUX, *OPT_PUBLISHED])
     ap.add_argument("--n-traj", type=int, default=256, help="C5 trajectories per point")
+    ap.add_argument("--c5-shards", type=int, default=0,
+                    help="C5: time rank --c5-rank's shard of an N-way split on this one GPU (0: off)")
+    ap.add_argument("--c5-rank", type=int, default=0)
+    ap.add_argument("--c5-order", default="balanced", choices=["balanced", "omega"],
+                    help="C5 grid point order (sweeps.blockade_grid_3atom)")
     ap.add_argument("--ladder", type=int, default=-1,
                     help="C5 ladder levels (0: exact jump times; -1: trajectories.DEFAULT_LADDER)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test: no GPU
@@ -587,6 +678,8 @@ def main():
         return run_stub(ws, rank, local, pg)
     if args.workload == "c5":
         return run_c5(args, ws, rank, local, pg)
+    if args.workload == "c1":
+        return run_c1(args, ws, rank, local, pg)
     if args.workload in AUX:
         return run_aux(args, ws, rank, local, pg)
     if args.workload in OPT_PUBLISHED:

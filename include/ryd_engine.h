@@ -225,6 +225,11 @@ typedef struct ryd_traj_desc {
 /* Set by ryd_mixed_phase: the reference's mixed-state phase penalty is not a function
  * of rho at the checked precision (LAPACK eigenvector gauge, see below). */
 #define RYD_STATUS_GAUGE_UNSTABLE 64u
+/* Set by ryd_run_trajectories in exact mode (RYD_T_EXACT): the point's |Omega| or Delta
+ * changes between segments, or its H_eff eigen-decomposition is unconverged or
+ * ill-conditioned (near an exceptional point); the point ran on the L = 16 ladder walk
+ * instead (jump times resolved to segment / 2^16).  A warning, not a failure. */
+#define RYD_STATUS_EXACT_FALLBACK 128u
 
 typedef struct ryd_batch_desc {
     int32_t abi_version;     /* = RYD_ABI_VERSION */

@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import warnings
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -34,6 +35,7 @@ STATUS_NONFINITE, STATUS_STEP_CAP, STATUS_BAD_INPUT = 1, 2, 4
 STATUS_FAIL_MASK = 7                      # kernel failures; the bits below are warnings
 STATUS_WEAK_BLOCKADE, STATUS_DARK_STATE_SIGN, STATUS_OMEGA_RANGE = 8, 16, 32
 STATUS_GAUGE_UNSTABLE = 64
+STATUS_EXACT_FALLBACK = 128               # C5 exact mode: this point ran on the L = 16 ladder
 # ryd_mixed_phase output rows
 MP = dict(V0=0, CTRL=8, PENALTY=9, SPREAD=10)
 MP_WIDTH = 11
@@ -178,7 +180,19 @@ def lapack_pool_copies(n_threads: int) -> int:
     """Copies the epilogue asks for: RYD_LAPACK_POOL (0 = off, N = at most N copies),
     default min(n_threads, 8)."""
     env = os.environ.get("RYD_LAPACK_POOL")
-    cap = LAPACK_POOL_DEFAULT if env is None or env.strip() == "" else int(env)
+    cap = LAPACK_POOL_DEFAULT
+    if env is not None and env.strip() != "":
+        try:
+            cap = int(env)
+        except ValueError:
+            warnings.warn(f"RYD_LAPACK_POOL={env!r} is not an integer copy cap (0 = off, N = at most N "
+                          f"copies): using the default {LAPACK_POOL_DEFAULT}")
+            cap = LAPACK_POOL_DEFAULT
+        if cap == 1:
+            # before round 3 the variable was an on/off switch and '1' meant 'on'; one copy
+            # would serialise the epilogue like no pool at all, so '1' keeps the default on
+            warnings.warn("RYD_LAPACK_POOL=1 is read as 'on' (the default cap); use 0 to turn the pool off")
+            cap = LAPACK_POOL_DEFAULT
     return max(0, min(n_threads, cap))
 
 

@@ -23,6 +23,7 @@ reference's DE trajectory exactly (still on the GPU engine).
 from __future__ import annotations
 
 import hashlib
+import inspect
 import json
 import os
 import time
@@ -395,12 +396,34 @@ def default_batch_evaluator(simulation_inputs, n: int, include_noise: bool, over
     return m, br.ok
 
 
+def _check_evaluator_accepts(evaluator, ev_kw: Dict[str, Any]) -> None:
+    """Raise TypeError if ``evaluator`` takes neither the keywords of ``ev_kw`` nor **kwargs
+    (e.g. cost='process_fidelity' with an evaluator that cannot supply avg_gate_fidelity)."""
+    try:
+        sig = inspect.signature(evaluator)
+    except (TypeError, ValueError):          # builtins / C callables: nothing to check
+        return
+    params = sig.parameters.values()
+    if any(p.kind is inspect.Parameter.VAR_KEYWORD for p in params):
+        return
+    names = {p.name for p in params if p.kind in (inspect.Parameter.POSITIONAL_OR_KEYWORD,
+                                                  inspect.Parameter.KEYWORD_ONLY)}
+    missing = sorted(k for k in ev_kw if k not in names)
+    if missing:
+        raise TypeError(f"batch evaluator {getattr(evaluator, '__name__', evaluator)!r} does not accept "
+                        f"{missing}: the requested cost needs an evaluator that supplies them")
+
+
 def _evaluate_rows(evaluator, si, X_over: Dict[str, Any], n: int, include_noise: bool, apparatus_rows,
                    **ev_kw):
     """Evaluate a population; if the whole batch raises (the reference's per-call
     exception path), fall back to one candidate at a time so only the failing
     candidates get the failure cost.  ``ev_kw`` (e.g. process_fidelity=True) goes to
-    the evaluator only when given, so evaluators without those keywords still work."""
+    the evaluator only when given, so evaluators without those keywords still work -- and an
+    evaluator that cannot take them is refused up front (a TypeError caught below would
+    otherwise give every candidate the failure cost silently)."""
+    if ev_kw:
+        _check_evaluator_accepts(evaluator, ev_kw)
     try:
         return evaluator(si, n, include_noise, X_over, **ev_kw, **apparatus_rows)
     except Exception:

@@ -6,7 +6,7 @@ Also defines the synthetic benchmark workloads of SURVEY.md §8d.
 from __future__ import annotations
 
 import warnings
-from typing import Optional
+from typing import Dict, Optional
 
 import numpy as np
 
@@ -142,25 +142,63 @@ def species_temperature_power_grid(n_T: int = 1000, n_P: int = 500, include_nois
                            include_noise=include_noise)
 
 
+# C1: one dim-3 LP-square point, Omega = 2 pi 5 MHz, V/Omega = 100, the LP
+# defaults Delta/Omega = 0.377371 and Omega tau = 4.29268, xi from compute_phase_shift_xi,
+# one collapse operator sqrt(gamma) |1><r| (x) I with gamma = 1/140 us (Rb87 n = 70)
+C1_OMEGA = 2 * np.pi * 5e6
+C1_V_OVER_OMEGA = 100.0
+C1_GAMMA = 1.0 / 140e-6
+
+
+def c1_point() -> Dict[str, float]:
+    """The C1 point's physics inputs (the columns the kernel reads)."""
+    from . import protocols as PR
+    Om = C1_OMEGA
+    Dl = PR.LP_DELTA_OVER_OMEGA_DEFAULT * Om
+    tau = PR.LP_OMEGA_TAU_DEFAULT / Om
+    xi = complex(PR.compute_phase_shift_xi(np.array([Dl]), np.array([Om]), np.array([tau]))[0])
+    return dict(Omega=Om, V=C1_V_OVER_OMEGA * Om, Delta=Dl, tau=tau, xi=xi, gamma=C1_GAMMA)
+
+
+def c1_params() -> np.ndarray:
+    """C1 packed for the engine: atom A's |1><r| channel only (the c_op acts on atom A)."""
+    from . import engine as E
+    c = c1_point()
+    P = E.N.P
+    p = np.zeros((E.N.NPARAM, 1))
+    p[P["OMEGA"]], p[P["DELTA"]], p[P["V"]], p[P["TAU"]] = c["Omega"], c["Delta"], c["V"], c["tau"]
+    p[P["XI_RE"]], p[P["XI_IM"]] = c["xi"].real, c["xi"].imag
+    p[P["AREA_CORR"]] = 1.0
+    p[P["G1_A"]] = c["gamma"]
+    return p
+
+
 C5_SHAPE = (64, 64)                # Omega x V/Omega
 C5_POINTS = 64 * 64
 
 
 def blockade_grid_3atom(n_omega: int = 64, n_vo: int = 64, include_noise: bool = True,
-                        point_slice: Optional[slice] = None) -> PH.DerivedBatch:
+                        point_slice: Optional[slice] = None, order: str = "balanced") -> PH.DerivedBatch:
     """C5: Omega/2pi in linspace(1, 10) MHz x V/Omega in logspace(10, 1000),
     LP square, medium apparatus.  Omega is set the physical way (480 nm leg power,
     Omega ∝ sqrt(P2)) and V/Omega through the atom spacing (V = C6/R^6, via
     spacing_factor), so the LP (Delta/Omega, Omega tau) lookup, xi and every noise rate
-    follow from the reference formulas per point.  Point order: Omega-major.  The
-    three-atom engine uses these two-atom columns for each atom and each pair."""
+    follow from the reference formulas per point.  Point order: V/Omega-major, Omega
+    fastest (round 4; was Omega-major).  A point's cost grows with its pulse length
+    tau ~ 1/Omega (more trajectories jump), so with Omega-major order the first eighth of
+    the grid -- rank 0's range shard at N = 8 -- carried twice the average work and set
+    the strong-scaling time; now every contiguous range spans the whole Omega axis
+    (``order="omega"``: the round-3 order).  The three-atom engine uses these two-atom
+    columns for each atom and each pair."""
     warnings.simplefilter("ignore")
     exc = medium_excitation()
     ref = PH.derive_batch(CF.LPSimulationInputs(excitation=exc), **_apparatus_kwargs(), include_noise=False)
     om0, V0 = ref["Omega"][0], ref["V"][0]
     om = 2 * np.pi * 1e6 * np.linspace(1, 10, n_omega)
     vo = np.logspace(1, 3, n_vo)
-    OM, VO = np.meshgrid(om, vo, indexing="ij")
+    if order not in ("balanced", "omega"):
+        raise ValueError("order must be 'balanced' or 'omega'")
+    OM, VO = np.meshgrid(om, vo, indexing="xy" if order == "balanced" else "ij")   # [V/Omega][Omega] | [Omega][V/Omega]
     OM, VO = OM.ravel(), VO.ravel()
     if point_slice is not None:
         OM, VO = OM[point_slice], VO[point_slice]
@@ -171,11 +209,11 @@ def blockade_grid_3atom(n_omega: int = 64, n_vo: int = 64, include_noise: bool =
                            overrides=dict(laser_2_power=p2))
 
 
-def c5_rank_shard(rank: int, world_size: int, include_noise: bool = True):
+def c5_rank_shard(rank: int, world_size: int, include_noise: bool = True, order: str = "balanced"):
     """Strong-scaling shard of the fixed 4096-point C5 grid: (batch, global offset of
     its first point) -- the offset keys the trajectories' random streams."""
     sl = range_shard(C5_POINTS, rank, world_size)
-    return blockade_grid_3atom(include_noise=include_noise, point_slice=sl), sl.start
+    return blockade_grid_3atom(include_noise=include_noise, point_slice=sl, order=order), sl.start
 
 
 def range_shard(n: int, rank: int, world_size: int) -> slice:

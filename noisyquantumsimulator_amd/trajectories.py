@@ -39,14 +39,18 @@ CHANNELS = ("|1><r|", "|0><r|", "P_r", "P_1")       # channel code = 4 * atom + 
 # resolved to segment / 2^L; at L = 16 the delay shifts the conditional state by
 # ~Omega tau / 2^(L+1) = 3e-5 per jump on the C5 points, against a standard error of
 # ~1e-2 at 256 trajectories.  DEFAULT_LADDER (None) picks exact times wherever they
-# apply and the L = 16 ladder for a shaped LP envelope.
+# apply and the L = 16 ladder for a shaped LP envelope.  In exact mode the library itself
+# sends a point whose |Omega| or Delta changes between segments (an LP square with
+# |xi| != 1), or whose H_eff eigenbasis is unconverged or ill-conditioned (near an
+# exceptional point), through the L = 16 ladder and marks it N.STATUS_EXACT_FALLBACK
+# (round 4: such points used to come back BAD_INPUT).
 DEFAULT_LADDER = None
 LADDER_WALK = 16
 
 
 def resolve_ladder(ladder_levels: Optional[int], protocol: str, shape: str = "square") -> int:
     """The ladder_levels a descriptor gets: ``None`` -> exact jump times, or the L = 16
-    ladder where exact mode does not apply (a shaped LP envelope)."""
+    ladder where exact mode cannot apply to any point (a shaped LP envelope)."""
     if ladder_levels is not None:
         return int(ladder_levels)
     return LADDER_WALK if (protocol == "lp_shaped" and shape != "square") else N.T["EXACT"]

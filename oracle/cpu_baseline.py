@@ -43,12 +43,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sample", type=int, default=96)
     ap.add_argument("--procs", type=int, default=8)
-    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     ap.add_argument("--n-traj", type=int, default=256)
     a = ap.parse_args()
     from noisyquantumsimulator_amd import sweeps as SW
     if a.workload == "c5":
         return main_c5(a, SW)
+    if a.workload == "c1":
+        return main_c1(a, SW)
     if a.workload == "c3":
         b = SW.pareto_tgate_grid()
         idx = np.linspace(0, b.n - 1, a.sample).astype(int)
@@ -112,6 +114,30 @@ def main_c5(a, SW):
                f"trajectories each through the oracle's exact-jump-time MCWF unravelling "
                f"(scipy expm + brentq, the same Philox streams); {a.procs} single-threaded "
                f"worker processes; {wall:.2f} s wall")))
+
+
+def main_c1(a, SW):
+    """C1: the single point's latency on one core, ZVODE (the QuTiP-like path) and expm."""
+    c = SW.c1_point()
+    s1r = O._trans(3, 1, 2)
+    spec = O.PointSpec(protocol="lp_square", Omega=c["Omega"], V=c["V"], Delta=c["Delta"], tau=c["tau"],
+                       xi=c["xi"], c_ops=[np.sqrt(c["gamma"]) * np.kron(s1r, np.eye(3))])
+    out = {}
+    for method in ("zvode", "expm"):
+        O.run_point(spec, method=method)                       # warm
+        ts = []
+        for _ in range(max(3, a.sample)):
+            t0 = time.perf_counter()
+            res = O.run_point(spec, method=method)
+            ts.append(time.perf_counter() - t0)
+        out[method] = (float(np.median(ts)) * 1e3, res)
+    fid = O.cz_fidelity(out["zvode"][1], 3)
+    print(json.dumps(dict(
+        value=out["zvode"][0], unit="ms", cores=1, kind="port", expm_ms=out["expm"][0],
+        avg_fidelity_zvode=float(fid[1]) if isinstance(fid, tuple) else None,
+        sample=f"the C1 point, median of {max(3, a.sample)} single-core calls per integrator: oracle "
+               f"ZVODE-Adams restatement of qutip.mesolve (atol 1e-10, rtol 1e-8, reference tlists) "
+               f"for the 4 basis inputs, 2 LP pulses; expm (exact) beside it")))
 
 
 if __name__ == "__main__":

@@ -196,18 +196,70 @@ def test_launch_shape_and_partition_independence(eng, ladder):
     np.testing.assert_array_equal(a.records, b.records[:, :256])     # a trajectory = its stream
     c = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5, **kw)
     np.testing.assert_array_equal(a.rho, c.rho)                         # deterministic
-    # device-side range shards with their global offsets == one batch (the exact kernel
-    # groups several points per wave: odd shard boundaries regroup them)
+    np.testing.assert_array_equal(a.se, c.se)
+    # device-side range shards with their global offsets == one batch (outputs, standard
+    # errors and the per-trajectory records bit for bit)
     outs = []
     for lo, hi in ((0, 3), (3, 4), (4, 8)):
-        db = TR.TrajectoryDeviceBatch(eng, p[:, lo:hi], "lp_square", n_traj=256, seed=5, point_offset=lo, **kw)
+        db = TR.TrajectoryDeviceBatch(eng, p[:, lo:hi], "lp_square", n_traj=256, seed=5, point_offset=lo,
+                                      records=True, **kw)
         db.launch()
         db.synchronize()
         outs.append(db.fetch())
         db.free()
     np.testing.assert_array_equal(np.concatenate([o.rho for o in outs]), a.rho)
+    np.testing.assert_array_equal(np.concatenate([o.se for o in outs]), a.se)
+    np.testing.assert_array_equal(np.concatenate([o.records for o in outs]), a.records)
     d = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=6, **kw)
     assert not np.array_equal(d.rho, a.rho)
+
+
+def test_exact_mode_falls_back_for_a_non_constant_schedule(eng):
+    """An LP square with |xi| != 1 has two different |Omega| segments: exact mode sends the
+    point through the L = 16 ladder (RYD_STATUS_EXACT_FALLBACK, not BAD_INPUT -- ADVICE r3)
+    while its neighbours stay exact."""
+    p = _c5([300, 1300, 2300], scale=30.0)
+    p[N.P["XI_RE"], 1] *= 0.8
+    p[N.P["XI_IM"], 1] *= 0.8
+    psi0 = TR.plus_state()
+    r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=2048, seed=11, ladder_levels=N.T["EXACT"])
+    assert r.status[1] == N.STATUS_EXACT_FALLBACK, r.status
+    assert r.status[0] == 0 and r.status[2] == 0
+    lad = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=2048, seed=11, ladder_levels=16)
+    np.testing.assert_array_equal(r.rho[1], lad.rho[1])              # the ladder kernel's own result
+    for i in range(3):
+        ref = O3.exact_rho(p[:, i], "lp_square", psi0)
+        d = np.abs(r.rho[i] - ref)
+        se = np.maximum(r.se[i], np.sqrt(np.abs(ref) / 2048))
+        assert np.all((d < 1e-9) | (d < 5.5 * se + 1e-8)), (i, (d / se).max())
+    q = p.copy()
+    q[4:12] = 0.0                                                    # and without noise: the pure ket
+    z = TR.run_trajectories(eng, q, "lp_square", psi0, n_traj=256, ladder_levels=N.T["EXACT"])
+    assert z.status[1] == N.STATUS_EXACT_FALLBACK
+    psi = O3.pure_ket(q[:, 1], "lp_square", psi0)
+    np.testing.assert_allclose(z.rho[1], np.outer(psi, psi.conj()), atol=1e-10, rtol=0)
+
+
+def test_exact_mode_guard_near_an_exceptional_point(eng):
+    """The single-atom block [[delta1 - i hgs, w], [w, -Delta - i hgr]] has an exceptional
+    point at Delta = -delta1, hgr - hgs = 2 w: there W e^{-i Lam t} W^T loses every digit.
+    Tuned to 1e-10 of it, the eigenbasis is flagged ill-conditioned, the point runs on the
+    ladder (RYD_STATUS_EXACT_FALLBACK) and still matches the 729 x 729 Liouvillian."""
+    p = _c5([1000, 2000])
+    i = 1
+    w = 0.5 * p[N.P["OMEGA"], i]
+    p[N.P["DELTA"], i] = -p[N.P["DELTA1"], i]
+    p[4:12, i] = 0.0
+    p[N.P["GPHI_A"], i] = p[N.P["GPHI_B"], i] = 4.0 * w * (1.0 + 1e-10)   # hgr = gphi / 2 = 2 w
+    psi0 = TR.plus_state()
+    r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=2048, seed=3, ladder_levels=N.T["EXACT"])
+    assert r.status[0] == 0
+    assert r.status[i] == N.STATUS_EXACT_FALLBACK, r.status
+    assert r.col("MEAN_JUMPS")[i] > 0.05
+    ref = O3.exact_rho(p[:, i], "lp_square", psi0)
+    d = np.abs(r.rho[i] - ref)
+    se = np.maximum(r.se[i], np.sqrt(np.abs(ref) / 2048))
+    assert np.all((d < 1e-9) | (d < 5.5 * se + 1e-8)), (d / se).max()
 
 
 @pytest.mark.parametrize("ladder", LADDERS)
@@ -244,3 +296,17 @@ def test_c5_full_grid_properties(eng, ladder):
         ref = O3.exact_rho(p[:, i], "lp_square", psi0)
         d = np.abs(r.rho[i] - ref)
         assert np.all((d < 1e-9) | (d < 5.5 * np.maximum(r.se[i], np.sqrt(np.abs(ref) / 256)) + 1e-8))
+    # the N = 8 strong-scaling shards (sweeps.c5_rank_shard) reproduce the full launch's rows
+    for rank in (0, 5):
+        b, off = SW.c5_rank_shard(rank, 8)
+        db = TR.TrajectoryDeviceBatch(eng, E.pack_params(b), "lp_square", n_traj=256, seed=20260215,
+                                      point_offset=off, ladder_levels=ladder)
+        db.launch()
+        db.synchronize()
+        o = db.fetch()
+        db.free()
+        np.testing.assert_array_equal(o.rho, r.rho[off:off + o.n])
+        np.testing.assert_array_equal(o.se, r.se[off:off + o.n])
+        # (ITER_EXEC counts the issued row-evaluations: scheduling-dependent in the exact kernel)
+        det = [N.TS[k] for k in ("MEAN_JUMPS", "FRAC_JUMPED", "MAX_JUMPS", "TRACE", "QUBIT_POP", "ITER_USEFUL")]
+        np.testing.assert_array_equal(o.summary[det], r.summary[det][:, off:off + o.n])

@@ -99,9 +99,13 @@ def test_c5_grid_and_shards():
     warnings.simplefilter("ignore")
     b = SW.blockade_grid_3atom()
     assert b.n == SW.C5_POINTS == 4096
-    vo = b["V_over_Omega"].reshape(64, 64)
-    np.testing.assert_allclose(vo[0], np.logspace(1, 3, 64), rtol=1e-9)
-    np.testing.assert_allclose(b["Omega"].reshape(64, 64)[:, 0] / (2e6 * np.pi), np.linspace(1, 10, 64), rtol=1e-12)
+    vo = b["V_over_Omega"].reshape(64, 64)                 # [V/Omega][Omega]: Omega fastest
+    np.testing.assert_allclose(vo[:, 0], np.logspace(1, 3, 64), rtol=1e-9)
+    np.testing.assert_allclose(b["Omega"].reshape(64, 64)[0] / (2e6 * np.pi), np.linspace(1, 10, 64), rtol=1e-12)
+    # every N = 8 range shard spans the whole Omega axis (balanced strong scaling)
+    for r in range(8):
+        sl = SW.range_shard(4096, r, 8)
+        np.testing.assert_allclose(np.unique(b["Omega"][sl]) / (2e6 * np.pi), np.linspace(1, 10, 64), rtol=1e-12)
     p = E.pack_params(b)
     assert np.all(p[4:8] > 0)
     full = p
