@@ -477,6 +477,61 @@ FLOP_PER_KET_BLOCK_SEG = 40 + 99
 FLOP_PER_KET_BLOCK_BUILD = 650
 FLOP_PER_DIM4_TERM = 2 * 6 * (2 * 16 + 3) + 2 * 16 + 2 * 36
 FLOP_PER_COH_POINT_TERM = 2 * 332 + 2 * 332 + 148 + 144
+# lindblad4_prop_kernel (ryd_dim4_prop.inc): one triangle-generator application (apply_Lsym4:
+# the single-atom rows twice per output, 7 x (3+7+8+7+7+4) = 252 flops, the V term 32, the
+# Clenshaw add 21), one 21 x 21 squaring (9261 FMA), one segment (21^2 FMA + the frame), one
+# 6-vector term (36 + 12)
+FLOP_PER_D4_APPLY = 252 + 32 + 21
+FLOP_PER_D4_SQUARING = 2 * 21 ** 3
+FLOP_PER_D4_SEGMENT = 2 * 21 ** 2 + 4 * 21
+FLOP_PER_D4_VEC_TERM = 36 + 12
+
+
+def coh_prop_flops(params: np.ndarray, protocol: str) -> float:
+    """Algorithmic flops of coherence_prop_kernel (ryd_coh_prop.inc) on a batch: per sector
+    built (the (0,-1) sector, n = 10; (-1,-1) and (-1,+1), n = 4; (-1,0) too when the atoms
+    differ) n Chebyshev columns x the series terms at x / 2^s (332 / 148 / 144 flops per
+    term and column, as coherence_cheb_kernel's applications) + s squarings (n^3 complex
+    MACs) + per segment the inputs' n^2 complex MACs.  The kernel's own omega and s, restated
+    (h_bounds + the rate sum; s = ceil(log2(x / CP_XS)), CP_XS = 2); LP square and smooth JP
+    build once."""
+    from noisyquantumsimulator_amd import _native as N
+    P = N.P
+    Om, Dl, V, d1 = params[P["OMEGA"]], params[P["DELTA"]], params[P["V"]], params[P["DELTA1"]]
+    tau = params[P["TAU"]]
+    nseg, dt = (2, tau) if protocol == "lp_square" else (300, tau / 300)
+    Dl = Dl if protocol != "bangbang" else 0.0 * Dl
+    w = 0.5 * np.abs(Om)
+    e = [np.zeros_like(Om), d1, -Dl]
+    emin, emax = np.full_like(Om, np.inf), np.full_like(Om, -np.inf)
+    for a1 in range(3):
+        for a2 in range(a1, 3):
+            E = e[a1] + e[a2] + (V if a1 == a2 == 2 else 0.0)
+            r = w * ((a1 > 0) + (a2 > 0))
+            emin, emax = np.minimum(emin, E - r), np.maximum(emax, E + r)
+    rsum = np.abs(params[P["G1_A"]:P["GSC_A"] + 1]).sum(0) + np.abs(params[P["G1_B"]:P["GSC_B"] + 1]).sum(0)
+    x = (emax - emin + rsum) * dt
+    s = np.where(x > 2.0, np.ceil(np.log2(np.maximum(x, 1e-300) / 2.0)), 0.0)     # CP_XS
+    xs = x / 2.0 ** s
+    terms = np.array([_cheb_terms(v) + 1 for v in xs], float)
+    sym = np.all(params[P["G1_A"]:P["GSC_A"] + 1] == params[P["G1_B"]:P["GSC_B"] + 1], axis=0)
+    f = 0.0
+    for n, per_term, nin, on in ((10, 332, 2, np.ones_like(sym)), (10, 332, 2, ~sym), (4, 148, 1, np.ones_like(sym)),
+                                 (4, 144, 1, np.ones_like(sym))):
+        f += float((on * (n * terms * per_term + s * n ** 3 * 8 + nseg * nin * n * n * 8)).sum())
+    return f
+
+
+def _cheb_terms(x: float) -> int:
+    """ryd_engine.hip cheb_terms: series terms for tail < 1e-17."""
+    if x < 24.0:
+        t, k = 1.0, 0
+        while True:
+            k += 1
+            t *= 0.5 * x / k
+            if t < 1e-18 and k > x:
+                return k
+    return int(np.ceil(x + 12.0 * np.cbrt(x) + 10.0))
 AUX = {
     # name: (kernel, state rows per input (0: coherence), bytes per point, description)
     "shaped": ("lindblad_cheb_kernel", 25, 8 * 16 + 8 * 100 + 8 * 19 + 4,
@@ -491,9 +546,10 @@ AUX = {
     "ket_cheb": ("ket_cheb_kernel", 18, 8 * 15 + 8 * 72 + 8 * 19 + 4,
                  "C3 (Omega, Omega*tau) smooth-JP grid, 100k points x 300 segments, noise-free, the "
                  "Chebyshev state-vector ket kernel (method cheb_vector, the cross-check)"),
-    "coherence": ("coherence_cheb_kernel", 0, 8 * 15 + 8 * 20 + 4 + 4,
+    "coherence": ("coherence_prop_kernel", 0, 8 * 15 + 8 * 20 + 4 + 4,
                   "C2 (Omega, Delta) grid, LP square, full reference noise: the 6 upper qubit coherences "
-                  "of the process map (noise_models Kraus/CPTP), 4 sector launches"),
+                  "of the process map (noise_models Kraus/CPTP); one launch, one propagator per sector and "
+                  "point (RYD_COH_PROP=0: coherence_cheb_kernel, the per-lane Chebyshev over the pulse)"),
 }
 
 
@@ -541,22 +597,35 @@ def run_aux(args, ws, rank, local, pg):
     if args.workload == "coherence":
         coh, st = db.fetch()
         assert np.all(st == 0), "engine reported per-point failures"
-        # per-lane Chebyshev terms = those of the 25-dim vector kernel on the same segments
-        # (same omega * dt per segment): its NMV_USEFUL / 4 per point
-        rv = eng.run(params, protocol, "lindblad", method="cheb_vector")
-        terms = float(rv.col("NMV_USEFUL").sum()) / 4.0
-        flops = terms * FLOP_PER_COH_POINT_TERM
-        useful_exec = float(rv.col("NMV_EXEC").sum()) / max(float(rv.col("NMV_USEFUL").sum()), 1.0)
+        if os.environ.get("RYD_COH_PROP", "1") != "0":
+            kernel = "coherence_prop_kernel"
+            flops = coh_prop_flops(params, protocol)
+            useful_exec = None
+        else:
+            # per-lane Chebyshev terms = those of the 25-dim vector kernel on the same segments
+            # (same omega * dt per segment): its NMV_USEFUL / 4 per point
+            kernel = "coherence_cheb_kernel"
+            rv = eng.run(params, protocol, "lindblad", method="cheb_vector")
+            terms = float(rv.col("NMV_USEFUL").sum()) / 4.0
+            flops = terms * FLOP_PER_COH_POINT_TERM
+            useful_exec = float(rv.col("NMV_EXEC").sum()) / max(float(rv.col("NMV_USEFUL").sum()), 1.0)
     else:
         res = db.fetch()
         assert np.all(res.status == 0), "engine reported per-point failures"
         if args.workload == "ket":
             flops = (res.matvec_useful * FLOP_PER_KET_BLOCK_SEG
                      + float(res.col("NSQUARE").sum()) * FLOP_PER_KET_BLOCK_BUILD)
+        elif args.workload == "dim4" and os.environ.get("RYD_DIM4_PROP", "1") != "0":
+            kernel = "lindblad4_prop_kernel"           # NMV_USEFUL: terms per column; NMV_EXEC: 6-vector terms
+            nseg = 2
+            flops = (float(res.col("NMV_USEFUL").sum()) * 21 * FLOP_PER_D4_APPLY
+                     + float(res.col("NSQUARE").sum()) * FLOP_PER_D4_SQUARING
+                     + n * nseg * FLOP_PER_D4_SEGMENT + float(res.col("NMV_EXEC").sum()) * FLOP_PER_D4_VEC_TERM)
         else:
             per = {"shaped": FLOP_PER_MATVEC, "dim4": FLOP_PER_DIM4_TERM, "ket_cheb": FLOP_PER_KET_TERM}[args.workload]
             flops = res.matvec_useful * per
-        useful_exec = res.matvec_exec / max(res.matvec_useful, 1.0)
+        useful_exec = (res.matvec_exec / max(res.matvec_useful, 1.0)
+                       if kernel != "lindblad4_prop_kernel" else None)
     achieved_tf = flops / (k_ms * 1e-3) / 1e12
     achieved_gbs = bpp * n / (k_ms * 1e-3) / 1e9
     tr = _measured_traffic(args.workload, "aux", n, kernel)
@@ -570,7 +639,7 @@ def run_aux(args, ws, rank, local, pg):
         "roofline": {"bound": "fp64", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": tr["bytes_per_launch"] if tr else None,
                      "kernel": kernel, "kernel_ms": k_ms, "flops_per_launch": flops,
-                     "exec_over_useful": useful_exec},
+                     "flops_per_point": flops / n, "exec_over_useful": useful_exec},
         "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "bytes_per_launch": bpp * n},
     }

@@ -2312,6 +2312,9 @@ __global__ __launch_bounds__(BLOCK) void coherence_cheb_kernel(const double* __r
   else coherence_sector<PROTO, 3>(prm, n, ldp, out, ldo, status, n_steps, shape, b - b2);
 }
 
+#include "ryd_coh_prop.inc"
+#include "ryd_dim4_prop.inc"
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -2352,6 +2355,17 @@ bool use_sym16(const ryd_batch_desc* d) {
   const char* e = getenv("RYD_SYM16");
   if (e && e[0] == '0') return false;
   return d->dim == 3 && d->evolution == RYD_EVOL_LINDBLAD && d->method == RYD_METHOD_CHEBYSHEV &&
+         (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0 &&
+         (d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG ||
+          d->protocol == RYD_PROTO_SMOOTH_JP);
+}
+
+// dim 4, identical atoms, constant-|Omega| schedules: the triangle propagator kernel
+// (ryd_dim4_prop.inc); RYD_DIM4_PROP=0 keeps lindblad4_cheb_kernel (the cross-check)
+bool use_dim4_prop(const ryd_batch_desc* d) {
+  const char* e = getenv("RYD_DIM4_PROP");
+  if (e && e[0] == '0') return false;
+  return d->dim == 4 && d->evolution == RYD_EVOL_LINDBLAD && d->method == RYD_METHOD_CHEBYSHEV &&
          (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0 &&
          (d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG ||
           d->protocol == RYD_PROTO_SMOOTH_JP);
@@ -2546,6 +2560,20 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
     HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(DP_BLOCK), args, 0, stream));
     return RYD_OK;
   }
+  if (use_dim4_prop(d)) {
+    using PFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, double*, int64_t, uint32_t*,
+                         int, int);
+    PFn f = d->protocol == RYD_PROTO_LP_SQUARE ? lindblad4_prop_kernel<RYD_PROTO_LP_SQUARE>
+            : d->protocol == RYD_PROTO_SMOOTH_JP ? lindblad4_prop_kernel<RYD_PROTO_SMOOTH_JP>
+                                                  : lindblad4_prop_kernel<RYD_PROTO_BANGBANG>;
+    const int64_t blocks = (n + D4_PPB - 1) / D4_PPB;
+    if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
+    int ns = d->n_steps, sh = d->shape;
+    void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
+                    (void*)&ldm, (void*)&dstat, (void*)&ns, (void*)&sh};
+    HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(BLOCK), args, 0, stream));
+    return RYD_OK;
+  }
   if (use_sym16(d)) {
     using SFn = void (*)(const double*, int64_t, int64_t, double*, int64_t, double*, int64_t, uint32_t*,
                          int, int);
@@ -2574,9 +2602,23 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
   return RYD_OK;
 }
 
+// RYD_COH_PROP=0 selects coherence_cheb_kernel for every protocol (A/B and cross-check runs)
+bool coh_prop_enabled() {
+  const char* e = getenv("RYD_COH_PROP");
+  return !(e && e[0] == '0');
+}
+
 template <int PROTO>
 int launch_coherences_proto(const double* dp, int64_t n, int64_t ldp, double* dc, int64_t ldc,
                             uint32_t* dstat, int ns, int sh, hipStream_t stream) {
+  if (PROTO != RYD_PROTO_LP_SHAPED && coh_prop_enabled()) {   // one propagator per sector (ryd_coh_prop.inc)
+    const int64_t blocks = (n + CP_NR - 1) / CP_NR;
+    if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
+    void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&dc, (void*)&ldc, (void*)&dstat, (void*)&ns, (void*)&sh};
+    HIPCHK(hipLaunchKernel((const void*)coherence_prop_kernel<PROTO>, dim3((unsigned)blocks), dim3(BLOCK), args, 0,
+                           stream));
+    return RYD_OK;
+  }
   const int64_t nb2 = (2 * n + BLOCK - 1) / BLOCK, nb1 = (n + BLOCK - 1) / BLOCK;
   const int64_t b0 = nb2, b1 = 2 * nb2, b2 = 2 * nb2 + nb1, blocks = 2 * nb2 + 2 * nb1;
   if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");

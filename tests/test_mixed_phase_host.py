@@ -80,6 +80,35 @@ def test_phases_bit_identical_to_scipy_eigh():
             assert np.angle(U[IDX[x], int(np.argmax(w))]) == ph[i, x]      # bit for bit
 
 
+def test_diagonal_rho_shortcut_bit_identical_to_scipy_eigh():
+    """ryd_mixed_phase skips LAPACK for an exactly diagonal rho whose entry at the input's
+    index is the strict maximum (the |00> output of every point): the component it returns,
+    1 + 0j, must be what scipy.linalg.eigh (zheevr) gives on the same matrix, bit for bit,
+    and the other three inputs still go through LAPACK."""
+    rng = np.random.default_rng(3)
+    blocks = [S for _, S in _noisy_fixture_states()]
+    n = 200
+    st = np.zeros((25, 4 * n))
+    for i in range(n):
+        st[:, 4 * i:4 * i + 4] = blocks[i % len(blocks)]
+        R = np.zeros(25)
+        R[0] = 1.0 - rng.integers(0, 4) * 2.0 ** -53 if i % 3 else rng.uniform(0.5, 1.0)
+        if i % 2:                                  # other populations below it (still diagonal)
+            R[6], R[12] = rng.uniform(0, 0.4 * R[0], 2)
+        st[:, 4 * i] = R                            # |00>: e00 (x) e00 (+ diagonal mass)
+    ph, _ = E.mixed_phase(st, n, 3, gauge_check=False)
+    for i in range(n):
+        rho = expand_like_host(st[:, 4 * i])
+        assert np.count_nonzero(rho - np.diag(np.diag(rho))) == 0
+        w, U = sla.eigh(rho)
+        v = U[IDX[0], int(np.argmax(w))]
+        assert v.real == 1.0 and v.imag == 0.0 and not np.signbit(v.imag)
+        assert np.angle(v) == ph[i, 0]
+        for x in (1, 2, 3):                         # LAPACK path unchanged
+            w, U = sla.eigh(expand_like_host(st[:, 4 * i + x]))
+            assert np.angle(U[IDX[x], int(np.argmax(w))]) == ph[i, x]
+
+
 def test_penalty_formula_matches_reference_scalars():
     rng = np.random.default_rng(5)
     ph = rng.uniform(-np.pi, np.pi, size=(500, 4))
