@@ -479,11 +479,11 @@ FLOP_PER_DIM4_TERM = 2 * 6 * (2 * 16 + 3) + 2 * 16 + 2 * 36
 FLOP_PER_COH_POINT_TERM = 2 * 332 + 2 * 332 + 148 + 144
 # lindblad4_prop_kernel (ryd_dim4_prop.inc): one triangle-generator application (apply_Lsym4:
 # the single-atom rows twice per output, 7 x (3+7+8+7+7+4) = 252 flops, the V term 32, the
-# Clenshaw add 21), one 21 x 21 squaring (9261 FMA), one segment (21^2 FMA + the frame), one
-# 6-vector term (36 + 12)
+# Clenshaw add 21), one 21 x 21 squaring (9261 FMA), one segment (21^2 + 6^2 FMA + the
+# frames), one 6-vector column term (36 + 12; the 6 x 6 squarings, <= 432 flops each, not counted)
 FLOP_PER_D4_APPLY = 252 + 32 + 21
 FLOP_PER_D4_SQUARING = 2 * 21 ** 3
-FLOP_PER_D4_SEGMENT = 2 * 21 ** 2 + 4 * 21
+FLOP_PER_D4_SEGMENT = 2 * 21 ** 2 + 4 * 21 + 2 * 6 ** 2 + 8
 FLOP_PER_D4_VEC_TERM = 36 + 12
 
 
@@ -616,11 +616,11 @@ def run_aux(args, ws, rank, local, pg):
             flops = (res.matvec_useful * FLOP_PER_KET_BLOCK_SEG
                      + float(res.col("NSQUARE").sum()) * FLOP_PER_KET_BLOCK_BUILD)
         elif args.workload == "dim4" and os.environ.get("RYD_DIM4_PROP", "1") != "0":
-            kernel = "lindblad4_prop_kernel"           # NMV_USEFUL: terms per column; NMV_EXEC: 6-vector terms
+            kernel = "lindblad4_prop_kernel"           # NMV_USEFUL / NMV_EXEC: terms per triangle / 6-vector column
             nseg = 2
             flops = (float(res.col("NMV_USEFUL").sum()) * 21 * FLOP_PER_D4_APPLY
                      + float(res.col("NSQUARE").sum()) * FLOP_PER_D4_SQUARING
-                     + n * nseg * FLOP_PER_D4_SEGMENT + float(res.col("NMV_EXEC").sum()) * FLOP_PER_D4_VEC_TERM)
+                     + n * nseg * FLOP_PER_D4_SEGMENT + float(res.col("NMV_EXEC").sum()) * 6 * FLOP_PER_D4_VEC_TERM)
         else:
             per = {"shaped": FLOP_PER_MATVEC, "dim4": FLOP_PER_DIM4_TERM, "ket_cheb": FLOP_PER_KET_TERM}[args.workload]
             flops = res.matvec_useful * per
@@ -732,7 +732,7 @@ def main():
     ap.add_argument("--c5-shards", type=int, default=0,
                     help="C5: time rank --c5-rank's shard of an N-way split on this one GPU (0: off)")
     ap.add_argument("--c5-rank", type=int, default=0)
-    ap.add_argument("--c5-order", default="balanced", choices=["balanced", "omega"],
+    ap.add_argument("--c5-order", default="blocked", choices=["blocked", "balanced", "omega"],
                     help="C5 grid point order (sweeps.blockade_grid_3atom)")
     ap.add_argument("--ladder", type=int, default=-1,
                     help="C5 ladder levels (0: exact jump times; -1: trajectories.DEFAULT_LADDER)")

@@ -34,7 +34,7 @@ for nm, c in zip(names, cols):
     v = r.col(c)
     print(f"  {nm:15s} mean {v.mean():10.0f}  ({100 * v.mean() / tot.mean():5.1f} %)  p90 {np.percentile(v, 90):10.0f}")
 print(f"  {'total':15s} mean {tot.mean():10.0f}  max {tot.max():10.0f}")
-if L == 0 and os.environ.get("RYD_T_WG", "1") != "0":      # traj3w_kernel: the eigen-decomposition's share of pass 1
+if L == 0 and os.environ.get("RYD_T_WG", "0") == "1":      # traj3w_kernel: the eigen-decomposition's share of pass 1
     v = r.col("NLADDER")
     print(f"  (of pass 1: eigen-decomposition mean {v.mean():10.0f}  p90 {np.percentile(v, 90):10.0f})")
     trips, ev, jf = r.col("ITER_USEFUL"), r.col("NSQUARE"), r.col("ITER_EXEC")
