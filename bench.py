@@ -407,7 +407,7 @@ def run_c5(args, ws, rank, local, pg):
     it_exec = float(res.col("ITER_EXEC").sum())
     napply = float(res.col("RESERVED").sum())
     exact = db.desc.ladder_levels == TR.N.T["EXACT"]
-    wg = os.environ.get("RYD_T_WG", "1") != "0"
+    wg = os.environ.get("RYD_T_WG", "0") == "1"
     kernel = (("traj3w_kernel" if wg else "traj3e_kernel") if exact
               else ("traj3s_kernel" if napply > 0 else "traj3_kernel"))
     if exact:                                       # traj3e_kernel: evaluations + basis changes
@@ -732,7 +732,7 @@ def main():
     ap.add_argument("--c5-shards", type=int, default=0,
                     help="C5: time rank --c5-rank's shard of an N-way split on this one GPU (0: off)")
     ap.add_argument("--c5-rank", type=int, default=0)
-    ap.add_argument("--c5-order", default="blocked", choices=["blocked", "balanced", "omega"],
+    ap.add_argument("--c5-order", default="omega", choices=["omega", "blocked", "balanced"],
                     help="C5 grid point order (sweeps.blockade_grid_3atom)")
     ap.add_argument("--ladder", type=int, default=-1,
                     help="C5 ladder levels (0: exact jump times; -1: trajectories.DEFAULT_LADDER)")

@@ -178,27 +178,39 @@ C5_POINTS = 64 * 64
 
 
 def blockade_grid_3atom(n_omega: int = 64, n_vo: int = 64, include_noise: bool = True,
-                        point_slice: Optional[slice] = None, order: str = "balanced") -> PH.DerivedBatch:
+                        point_slice: Optional[slice] = None, order: str = "omega") -> PH.DerivedBatch:
     """C5: Omega/2pi in linspace(1, 10) MHz x V/Omega in logspace(10, 1000),
     LP square, medium apparatus.  Omega is set the physical way (480 nm leg power,
     Omega ∝ sqrt(P2)) and V/Omega through the atom spacing (V = C6/R^6, via
     spacing_factor), so the LP (Delta/Omega, Omega tau) lookup, xi and every noise rate
-    follow from the reference formulas per point.  Point order: V/Omega-major, Omega
-    fastest (round 4; was Omega-major).  A point's cost grows with its pulse length
-    tau ~ 1/Omega (more trajectories jump), so with Omega-major order the first eighth of
-    the grid -- rank 0's range shard at N = 8 -- carried twice the average work and set
-    the strong-scaling time; now every contiguous range spans the whole Omega axis
-    (``order="omega"``: the round-3 order).  The three-atom engine uses these two-atom
-    columns for each atom and each pair."""
+    follow from the reference formulas per point.  The point ORDER decides how a launch's
+    tail packs and how balanced the range shards are (the results do not depend on it):
+      * ``"omega"`` (the default): Omega-major.  The exact-jump kernel's waves pair point b
+        with its mirror, so the first-dispatched waves hold the Omega extremes -- the
+        longest walks -- and the short ones fill the tail (C5, N = 1: 0.51 ms); but rank 0's
+        eighth at N = 8 holds the 8 lowest Omega values (its shard 0.32 ms);
+      * ``"blocked"``: 8 blocks of 8 V/Omega rows (512 points each), Omega-major inside a
+        block: every range shard of N = 1, 2, 4, 8 ranks is a union of whole blocks spanning
+        the whole Omega axis (shard 0.28 ms), but long walks are dispatched last at N = 1
+        (0.72 ms);
+      * ``"balanced"``: V/Omega-major with Omega fastest (0.70 ms at N = 1).
+    (profiles/r04/c5_order/: per-wave start/end clocks of the three orders.)  The
+    three-atom engine uses these two-atom columns for each atom and each pair."""
     warnings.simplefilter("ignore")
     exc = medium_excitation()
     ref = PH.derive_batch(CF.LPSimulationInputs(excitation=exc), **_apparatus_kwargs(), include_noise=False)
     om0, V0 = ref["Omega"][0], ref["V"][0]
     om = 2 * np.pi * 1e6 * np.linspace(1, 10, n_omega)
     vo = np.logspace(1, 3, n_vo)
-    if order not in ("balanced", "omega"):
-        raise ValueError("order must be 'balanced' or 'omega'")
-    OM, VO = np.meshgrid(om, vo, indexing="xy" if order == "balanced" else "ij")   # [V/Omega][Omega] | [Omega][V/Omega]
+    if order not in ("blocked", "balanced", "omega"):
+        raise ValueError("order must be 'omega', 'blocked' or 'balanced'")
+    if order == "blocked" and n_vo % 8 == 0:
+        # [block][Omega][V/Omega within the block]
+        VB = vo.reshape(8, n_vo // 8)
+        OM = np.broadcast_to(om[None, :, None], (8, n_omega, n_vo // 8))
+        VO = np.broadcast_to(VB[:, None, :], (8, n_omega, n_vo // 8))
+    else:                                                        # [Omega][V/Omega] | [V/Omega][Omega]
+        OM, VO = np.meshgrid(om, vo, indexing="ij" if order == "omega" else "xy")
     OM, VO = OM.ravel(), VO.ravel()
     if point_slice is not None:
         OM, VO = OM[point_slice], VO[point_slice]
@@ -209,7 +221,7 @@ def blockade_grid_3atom(n_omega: int = 64, n_vo: int = 64, include_noise: bool =
                            overrides=dict(laser_2_power=p2))
 
 
-def c5_rank_shard(rank: int, world_size: int, include_noise: bool = True, order: str = "balanced"):
+def c5_rank_shard(rank: int, world_size: int, include_noise: bool = True, order: str = "omega"):
     """Strong-scaling shard of the fixed 4096-point C5 grid: (batch, global offset of
     its first point) -- the offset keys the trajectories' random streams."""
     sl = range_shard(C5_POINTS, rank, world_size)

@@ -99,13 +99,24 @@ def test_c5_grid_and_shards():
     warnings.simplefilter("ignore")
     b = SW.blockade_grid_3atom()
     assert b.n == SW.C5_POINTS == 4096
-    vo = b["V_over_Omega"].reshape(64, 64)                 # [V/Omega][Omega]: Omega fastest
-    np.testing.assert_allclose(vo[:, 0], np.logspace(1, 3, 64), rtol=1e-9)
-    np.testing.assert_allclose(b["Omega"].reshape(64, 64)[0] / (2e6 * np.pi), np.linspace(1, 10, 64), rtol=1e-12)
-    # every N = 8 range shard spans the whole Omega axis (balanced strong scaling)
+    # the default order: Omega-major, V/Omega fastest
+    np.testing.assert_allclose(b["V_over_Omega"].reshape(64, 64)[0], np.logspace(1, 3, 64), rtol=1e-9)
+    np.testing.assert_allclose(b["Omega"].reshape(64, 64)[:, 0] / (2e6 * np.pi), np.linspace(1, 10, 64), rtol=1e-12)
+    # blocked order: [8 V/Omega blocks][64 Omega][8 V/Omega in the block]
+    bb = SW.blockade_grid_3atom(order="blocked")
+    vo = bb["V_over_Omega"].reshape(8, 64, 8)
+    np.testing.assert_allclose(vo[:, 0, :].ravel(), np.logspace(1, 3, 64), rtol=1e-9)
+    np.testing.assert_allclose(bb["Omega"].reshape(8, 64, 8)[0, :, 0] / (2e6 * np.pi), np.linspace(1, 10, 64),
+                               rtol=1e-12)
+    om = bb["Omega"].reshape(8, 64, 8)
+    assert np.all(np.diff(om, axis=1) > 0)                  # low Omega first in a block
+    # every N = 8 range shard of the blocked order spans the whole Omega axis
     for r in range(8):
         sl = SW.range_shard(4096, r, 8)
-        np.testing.assert_allclose(np.unique(b["Omega"][sl]) / (2e6 * np.pi), np.linspace(1, 10, 64), rtol=1e-12)
+        np.testing.assert_allclose(np.unique(bb["Omega"][sl]) / (2e6 * np.pi), np.linspace(1, 10, 64), rtol=1e-12)
+    # the same point set in every order
+    key = lambda x: np.lexsort((x["V_over_Omega"], x["Omega"]))
+    np.testing.assert_array_equal(b["Omega"][key(b)], bb["Omega"][key(bb)])
     p = E.pack_params(b)
     assert np.all(p[4:8] > 0)
     full = p
