@@ -173,7 +173,7 @@ def scipy_zheevr() -> int:
 
 
 _pool_size: Optional[int] = None
-LAPACK_POOL_DEFAULT = 8     # copies (the C side caps at 8: each holds a glibc link namespace)
+LAPACK_POOL_DEFAULT = 8     # copies (each holds a glibc link namespace; RYD_LAPACK_POOL raises it, C cap 15)
 
 
 def lapack_pool_copies(n_threads: int) -> int:
