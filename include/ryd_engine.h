@@ -353,10 +353,28 @@ int ryd_mixed_phase(void* zheevr, int dim, const double* state, int64_t n, int64
  * lock.  *n_loaded = pool size (loading stops quietly when namespaces or static TLS run
  * out); an error only if no copy could be loaded.  PROCESS-WIDE SIDE EFFECT: each copy
  * occupies a glibc link namespace and static-TLS space for the life of the process, so
- * copies are capped at 8 and loading is attempted once per process: later calls return
+ * copies are capped at 15 and loading is attempted once per process: later calls return
  * the first attempt's outcome (partial or failed) and never call dlmopen again. */
 int ryd_lapack_pool(void* ref_zheevr, const char* path, const char* zheevr_symbol,
                     const char* threads_symbol, int copies, int* n_loaded);
+
+/* The generic evolve_state seam (RG/simulation.py:647-690: mesolve(H, psi0, tlist, c_ops)
+ * for any H and c_ops, SURVEY.md §8b's GENERIC_SCHEDULE with a generic jump-operator
+ * list).  For each of n problems: n_seg piecewise-constant segments (H_s, dt_s), n_ops
+ * jump operators L_k shared by the segments, evolve
+ *     drho/dt = -i [H_s, rho] + sum_k (L_k rho L_k^dag - {L_k^dag L_k, rho} / 2)
+ * (or, ket != 0 and n_ops == 0, dpsi/dt = -i H_s psi) from state0 and write the final
+ * state.  Complex arrays are interleaved (re, im), matrices row-major:
+ *   H [n][n_seg][dim][dim], dt [n][n_seg] (segments with dt <= 0 are skipped),
+ *   ops [n][n_ops][dim][dim] (nullable when n_ops == 0),
+ *   state0 / state_out [n][dim][dim] (density) or [n][dim] (ket).
+ * dim <= 16, n_ops <= 32, at most 1024 nonzero operator entries per problem.  Exact
+ * propagation per segment (Chebyshev series of exp(dt L), tail < 1e-17) on the handle's
+ * first device; host buffers, blocking.  status[i]: RYD_STATUS_STEP_CAP (omega dt above
+ * 2e6 rad in one segment; the state is the last one reached), RYD_STATUS_NONFINITE. */
+int ryd_evolve_generic(ryd_handle* h, int dim, int n_seg, int n_ops, int64_t n, int ket,
+                       const double* H, const double* dt, const double* ops,
+                       const double* state0, double* state_out, uint32_t* status);
 
 /* Timeline of the handle's last host-buffer call (ryd_run_batch / _coherences /
  * _trajectories).  Those calls keep a device workspace and a pinned host staging buffer

@@ -17,7 +17,8 @@ from .protocols import (JP_BANGBANG_OMEGA_TAU, JP_BANGBANG_PHASES, JP_BANGBANG_S
                         LP_DELTA_OVER_OMEGA_DEFAULT, LP_OMEGA_TAU_DEFAULT, LP_XI_DEFAULT,
                         SMOOTH_JP_DEFAULTS as SMOOTH_JP_PARAMS, compute_phase_shift_xi)
 from .simulation import (BatchResult, SimulationResult, compute_CZ_fidelity, compute_state_fidelity,
-                         mixed_phase_penalty, simulate_CZ_gate, simulate_CZ_gate_batch)
+                         evolve_state, evolve_state_batch, mixed_phase_penalty, simulate_CZ_gate,
+                         simulate_CZ_gate_batch)
 from .optimize_cz_gate import (JP_PHASES_DEFAULT, JP_SWITCHING_TIMES_DEFAULT, ApparatusConstraints,
                                OptimizationResult, SimulationCache, compute_cost, extract_metrics,
                                optimize_cz_gate, run_baseline)
@@ -30,7 +31,7 @@ from .calibration import calibrate_cz, load_calibration, write_calibration
 __all__ = [
     # simulate / analyse (RG/simulation.py)
     "simulate_CZ_gate", "simulate_CZ_gate_batch", "SimulationResult", "BatchResult",
-    "compute_CZ_fidelity", "compute_state_fidelity", "mixed_phase_penalty",
+    "compute_CZ_fidelity", "compute_state_fidelity", "mixed_phase_penalty", "evolve_state", "evolve_state_batch",
     # inputs (RG/configurations.py)
     "TwoPhotonExcitationConfig", "NoiseSourceConfig", "LPSimulationInputs", "JPSimulationInputs",
     "SmoothJPSimulationInputs", "LaserParameters", "AtomicConfiguration",

@@ -60,7 +60,7 @@ EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary
             "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
             "ryd_run_trajectories", "ryd_run_trajectories_device",
             "ryd_mixed_phase", "ryd_lapack_pool", "ryd_last_timeline", "ryd_mark", "ryd_mark_elapsed",
-            "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize")
+            "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize", "ryd_evolve_generic")
 
 
 class BatchDesc(ctypes.Structure):
@@ -139,6 +139,8 @@ def load() -> ctypes.CDLL:
         lib.ryd_memcpy_h2d.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]
         lib.ryd_memcpy_d2h.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_size_t]
         lib.ryd_synchronize.argtypes = [vp]
+        lib.ryd_evolve_generic.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, dp, dp,
+                                           dp, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
         if lib.ryd_abi_version() != RYD_ABI_VERSION:
             raise EngineError("libryd_engine.so ABI version mismatch; rebuild it")
         if lib.ryd_param_count() != NPARAM or lib.ryd_summary_width() != NSUMMARY:

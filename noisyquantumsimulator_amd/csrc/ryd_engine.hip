@@ -35,6 +35,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <complex>
 #include <condition_variable>
 #include <mutex>
 #include <string>
@@ -3017,6 +3018,7 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
 
 // three-atom quantum-jump trajectories (BASELINE configs[4])
 #include "ryd_traj.inc"
+#include "ryd_generic.inc"
 
 // host epilogue: the reference's mixed-state controlled phase (ryd_mixed_phase)
 #include "ryd_epilogue.inc"
@@ -3277,6 +3279,21 @@ int ryd_run_trajectories(ryd_handle* h, const ryd_traj_desc* desc, const double*
     stats->reserved = 0;
   }
   return RYD_OK;
+}
+
+int ryd_evolve_generic(ryd_handle* h, int dim, int n_seg, int n_ops, int64_t n, int ket, const double* H,
+                       const double* dt, const double* ops, const double* state0, double* state_out,
+                       uint32_t* status) {
+  if (!h || h->dev.empty()) return fail(RYD_ERR_INVALID, "handle is NULL");
+  if (dim < 1 || dim > GN_DMAX || n_seg < 1 || n_ops < 0 || n_ops > (GN_ROWS - 1) / GN_DMAX || n < 0)
+    return fail(RYD_ERR_INVALID, "evolve_generic: need 1 <= dim <= 16, n_seg >= 1, 0 <= n_ops <= 32, n >= 0");
+  if (ket && n_ops > 0)
+    return fail(RYD_ERR_INVALID, "evolve_generic: kets evolve without jump operators (with them, pass rho)");
+  if (n == 0) return RYD_OK;
+  if (n > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "evolve_generic: batch too large for one launch");
+  if (!H || !dt || !state0 || !state_out || !status || (n_ops > 0 && !ops))
+    return fail(RYD_ERR_INVALID, "evolve_generic: NULL buffer");
+  return run_generic(h->dev[0], h->stream[0], dim, n_seg, n_ops, n, ket, H, dt, ops, state0, state_out, status);
 }
 
 int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* desc, const double* d_params,

@@ -304,6 +304,37 @@ class Engine:
         return coh, status
 
 
+    def evolve_generic(self, H: np.ndarray, dt: np.ndarray, state0: np.ndarray,
+                       ops: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """The generic evolve_state seam (ryd_evolve_generic; RG/simulation.py:647-690) for
+        a batch: H (n, n_seg, d, d) piecewise-constant Hamiltonians, dt (n, n_seg), state0
+        (n, d) kets or (n, d, d) density matrices, ops (n, K, d, d) jump operators (kets
+        only without them).  Returns (final states, status (n,) uint32)."""
+        H = np.ascontiguousarray(H, dtype=np.complex128)
+        if H.ndim != 4 or H.shape[2] != H.shape[3]:
+            raise ValueError("H must have shape (n, n_seg, d, d)")
+        n, n_seg, d = H.shape[0], H.shape[1], H.shape[2]
+        dt = np.ascontiguousarray(np.broadcast_to(np.asarray(dt, dtype=np.float64), (n, n_seg)))
+        state0 = np.ascontiguousarray(state0, dtype=np.complex128)
+        ket = state0.shape == (n, d)
+        if not ket and state0.shape != (n, d, d):
+            raise ValueError("state0 must have shape (n, d) or (n, d, d)")
+        K = 0
+        if ops is not None:
+            ops = np.ascontiguousarray(ops, dtype=np.complex128)
+            if ops.ndim != 4 or ops.shape[0] != n or ops.shape[2:] != (d, d):
+                raise ValueError("ops must have shape (n, K, d, d)")
+            K = ops.shape[1]
+        out = np.zeros_like(state0)
+        status = np.zeros(n, dtype=np.uint32)
+        dptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        N.check(self.lib.ryd_evolve_generic(
+            self.handle, d, n_seg, K, n, 1 if ket else 0, dptr(H), dptr(dt),
+            dptr(ops) if K > 0 else None, dptr(state0), dptr(out),
+            status.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))))
+        return out, status
+
+
 class DeviceBatch:
     """Inputs resident in HBM on one device slot, for timed re-runs (bench.py)."""
 

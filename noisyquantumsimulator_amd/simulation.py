@@ -322,6 +322,61 @@ def _engine(devices=None):
     return _ENGINES[key]
 
 
+def _as_array(x) -> np.ndarray:
+    """A dense complex array from an ndarray or a Qobj-like object (anything with .full())."""
+    return np.asarray(x.full() if hasattr(x, "full") else x, dtype=np.complex128)
+
+
+def evolve_state(H, psi0, tlist, c_ops=None, options=None, *, devices=None) -> np.ndarray:
+    """The reference's generic time-evolution helper (RG/simulation.py:647-690:
+    ``mesolve(H, psi0, tlist, c_ops=c_ops, options=options).states[-1]``) on the GPU
+    (``ryd_evolve_generic``): H constant from tlist[0] to tlist[-1], any jump operators.
+    Like mesolve, a ket without collapse operators evolves as a ket (its phase kept) and
+    otherwise the result is the density matrix.  ``options`` (atol / rtol / nsteps) is
+    accepted for signature compatibility and unused: each segment is propagated exactly
+    (Chebyshev series, tail < 1e-17).  H, psi0, c_ops: arrays or Qobj-like objects;
+    returns an ndarray ((d,) ket or (d, d) density matrix)."""
+    del options
+    Hm = _as_array(H)
+    v = _as_array(psi0)
+    tl = np.asarray(tlist, dtype=np.float64)
+    T = float(tl[-1] - tl[0]) if tl.size else 0.0
+    ops = [_as_array(c) for c in (c_ops or [])]
+    return evolve_state_batch(Hm[None], v[None], np.array([T]), [ops] if ops else None, devices=devices)[0]
+
+
+def evolve_state_batch(H, psi0, T, c_ops=None, *, devices=None) -> np.ndarray:
+    """Many independent evolve_state problems in one launch.  H (n, d, d) or, for
+    piecewise-constant schedules, (n, n_seg, d, d) with T (n, n_seg) segment lengths;
+    psi0 (n, d) kets or (n, d, d) density matrices; c_ops None or (n, K, d, d) (or a list of
+    per-problem lists of K operators).  Kets with c_ops are evolved as |psi><psi|.  Raises
+    EngineError for a failed problem (step cap: omega * dt > 2e6 rad in one segment;
+    non-finite)."""
+    from ._native import EngineError, STATUS_FAIL_MASK
+    H = np.asarray(H, dtype=np.complex128)
+    if H.ndim == 3:
+        H = H[:, None]
+    n, n_seg, d = H.shape[0], H.shape[1], H.shape[2]
+    T = np.asarray(T, dtype=np.float64).reshape(n, -1)
+    if T.shape[1] != n_seg:
+        raise ValueError("T must hold one length per segment")
+    v = np.asarray(psi0, dtype=np.complex128)
+    ops = None
+    if c_ops is not None and len(c_ops) > 0:
+        ops = np.asarray(c_ops, dtype=np.complex128)
+        if ops.ndim == 3:
+            ops = ops[None]
+        if ops.shape[1] == 0:
+            ops = None
+    if ops is not None and v.ndim == 2:                     # mesolve: a ket with c_ops -> rho
+        v = np.einsum("ni,nj->nij", v, v.conj())
+    out, status = _engine(devices).evolve_generic(H, T, v, ops)
+    bad = np.nonzero(status & STATUS_FAIL_MASK)[0]
+    if bad.size:
+        raise EngineError(f"evolve_state: problem {int(bad[0])} failed (status {int(status[bad[0]])})")
+    return out
+
+
 # gauge-check probes of the batch API (round 4: 4, as the optimiser and sweep drivers; was
 # engine.GAUGE_COPIES = 16).  A flagged point usually stops at the first probe; 4 probes miss an
 # unstable point with probability ~50-70 %, 16 with ~10-30 %, 64 with < 1 % (DESIGN.md §5) --

@@ -1,0 +1,107 @@
+"""The generic evolve_state seam (ryd_evolve_generic; SURVEY.md §8b's GENERIC_SCHEDULE with
+a generic jump-operator list; reference RG/simulation.py:647-690) against the oracle's
+evolve_state: expm of the column-stacked Liouvillian for density matrices, expm(-iHT) for
+kets (oracle/lindblad_oracle.py:183-246).  Tolerance 1e-10 absolute on entries of
+unit-trace states (1e-10 relative to the state's norm for the random problems)."""
+import warnings
+
+import numpy as np
+import pytest
+
+from noisyquantumsimulator_amd import _native as N
+from noisyquantumsimulator_amd import simulation as SIM
+from noisyquantumsimulator_amd import sweeps as SW
+from oracle import lindblad_oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def _c1():
+    c = SW.c1_point()
+    H1 = O.two_atom_hamiltonian(c["Omega"], c["Delta"], c["V"])
+    H2 = O.two_atom_hamiltonian(c["Omega"] * c["xi"], c["Delta"], c["V"])
+    cop = [np.sqrt(c["gamma"]) * O._two(O._trans(3, 1, 2), np.eye(3))]      # |1><r| (x) I
+    return c, H1, H2, cop
+
+
+def test_c1_lp_square_density_matrices():
+    """SURVEY §8d's C1 point as the reference runs it: two mesolve calls (H1, then H2 =
+    H(Omega xi)) with one collapse operator, from each computational-basis ket."""
+    warnings.simplefilter("ignore")
+    c, H1, H2, cop = _c1()
+    kets = list(O.initial_kets(3).values())
+    n = len(kets)
+    H = np.broadcast_to(np.stack([H1, H2])[None], (n, 2, 9, 9))
+    T = np.full((n, 2), c["tau"])
+    out = SIM.evolve_state_batch(H, np.stack(kets), T, [cop] * n)
+    for k, psi in enumerate(kets):
+        ref = O.evolve_state(H2, O.evolve_state(H1, psi, [0, c["tau"]], cop), [0, c["tau"]], cop)
+        assert np.max(np.abs(out[k] - ref)) < TOL
+        assert abs(np.trace(out[k]) - np.trace(ref)) < TOL
+
+
+def test_kets_keep_their_phase():
+    """No collapse operators: kets evolve as kets, global phase included (the CZ phase
+    fidelity reads it)."""
+    c, H1, H2, _ = _c1()
+    for psi in O.initial_kets(3).values():
+        out = SIM.evolve_state(H1, psi, np.linspace(0, c["tau"], 100))
+        ref = O.evolve_state(H1, psi, [0, c["tau"]])
+        assert out.shape == (9,)
+        assert np.max(np.abs(out - ref)) < TOL
+
+
+def test_mesolve_semantics_ket_with_collapse_ops_gives_rho():
+    c, H1, _, cop = _c1()
+    psi = O.initial_kets(3)["11"]
+    out = SIM.evolve_state(H1, psi, [0.0, 0.5 * c["tau"]], cop)
+    assert out.shape == (9, 9)
+    ref = O.evolve_state(H1, psi, [0.0, 0.5 * c["tau"]], cop)
+    assert np.max(np.abs(out - ref)) < TOL
+
+
+def test_dim4_two_atom_with_reference_collapse_operators():
+    """16-dimensional two-atom space (dim 4: |r+>, |r->) with the reference's c_op list."""
+    c = SW.c1_point()
+    H = O.two_atom_hamiltonian(c["Omega"], c["Delta"], c["V"], dim=4)
+    rates = {"gamma_r": 1 / 140e-6, "gamma_phi_laser": 2e3, "gamma_loss_background": 50.0,
+             "gamma_scatter_intermediate": 300.0, "mJ_leakage_rate": 1e3}
+    cops = O.collapse_operators(rates, dim=4)
+    psi = np.zeros(16, complex)
+    psi[5] = 1.0                                                            # |11>
+    out = SIM.evolve_state(H, psi, [0.0, c["tau"]], cops)
+    ref = O.evolve_state(H, psi, [0.0, c["tau"]], cops)
+    assert np.max(np.abs(out - ref)) < TOL
+
+
+@pytest.mark.parametrize("d,K", [(2, 1), (5, 3), (9, 2), (16, 2)])
+def test_random_dense_piecewise_problems(d, K):
+    """Dense random Hamiltonians and jump operators, three segments of random length."""
+    rng = np.random.default_rng(100 + d)
+    n, n_seg = 6, 3
+    A = rng.normal(size=(n, n_seg, d, d)) + 1j * rng.normal(size=(n, n_seg, d, d))
+    H = 0.5 * (A + np.conj(np.swapaxes(A, -1, -2))) * 3.0
+    L = (rng.normal(size=(n, K, d, d)) + 1j * rng.normal(size=(n, K, d, d))) * 0.4
+    T = rng.uniform(0.1, 2.0, size=(n, n_seg))
+    v = rng.normal(size=(n, d)) + 1j * rng.normal(size=(n, d))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    rho0 = np.einsum("ni,nj->nij", v, v.conj())
+    out = SIM.evolve_state_batch(H, rho0, T, L)
+    for i in range(n):
+        r = rho0[i]
+        for s in range(n_seg):
+            r = O.evolve_state(H[i, s], r, [0.0, T[i, s]], list(L[i]))
+        assert np.max(np.abs(out[i] - r)) < TOL * max(1.0, np.abs(r).max())
+    kets = SIM.evolve_state_batch(H, v, T)                                # no operators: kets
+    for i in range(n):
+        x = v[i]
+        for s in range(n_seg):
+            x = O.evolve_state(H[i, s], x, [0.0, T[i, s]])
+        assert np.max(np.abs(kets[i] - x)) < TOL
+
+
+def test_step_cap_is_a_failure():
+    c, H1, _, cop = _c1()
+    with pytest.raises(N.EngineError):
+        SIM.evolve_state(H1, O.initial_kets(3)["11"], [0.0, 1.0], cop)      # omega T ~ 1e10 rad

@@ -56,3 +56,9 @@ def test_library_loads_and_exports():
     assert lib.ryd_state_width(0, 3) == 25 and lib.ryd_state_width(1, 3) == 18
     assert lib.ryd_state_width(0, 4) == 36 and lib.ryd_state_width(1, 4) == 32
     assert lib.ryd_state_width(0, 5) == -1
+
+
+def test_evolve_generic_validates_before_any_gpu_call():
+    """ryd_evolve_generic rejects a NULL handle and bad sizes without touching a device."""
+    lib = N.load()
+    assert lib.ryd_evolve_generic(None, 9, 1, 0, 1, 1, None, None, None, None, None, None) == -1   # RYD_ERR_INVALID
