@@ -285,6 +285,19 @@ FLOP_PER_EIG_COEFFS = 8 * 66
 C5_BYTES_PER_POINT = 8 * 15 + 8 * (1458 + 729 + 10) + 4   # params read; rho, se, summary, status
 
 
+def _c1_hamiltonian(Om: complex, Dl: float, V: float) -> np.ndarray:
+    """The two-atom dim-3 H of RG/hamiltonians.py:584-1274 for the generic-seam timing:
+    sum_atoms [(Om/2)|r><1| + h.c. - Dl P_r] + V P_rr (levels 0, 1, r)."""
+    h1 = np.zeros((3, 3), complex)
+    h1[2, 1] = Om / 2
+    h1[1, 2] = np.conj(Om) / 2
+    h1[2, 2] = -Dl
+    I = np.eye(3)
+    prr = np.zeros((9, 9))
+    prr[8, 8] = 1.0
+    return np.kron(h1, I) + np.kron(I, h1) + V * prr
+
+
 def run_c1(args, ws, rank, local, pg):
     """C1: ONE dim-3 LP-square point with one collapse operator, as a
     single-point latency -- what every unmodified per-point caller of the reference
@@ -337,6 +350,26 @@ def run_c1(args, ws, rank, local, pg):
             br = SIM.simulate_CZ_gate_batch(si, 1, include_noise=True, return_states=True)
             parts.append(br.timings)
     med = lambda v: float(np.median(v))
+    # the generic evolve_state seam on the same C1 point (the reference's two mesolve calls
+    # per basis input, H1 then H2 = H(Omega xi), one collapse operator): 4 problems, 2 segments
+    c1 = SW.c1_point()
+    H1 = _c1_hamiltonian(c1["Omega"], c1["Delta"], c1["V"])
+    H2 = _c1_hamiltonian(c1["Omega"] * c1["xi"], c1["Delta"], c1["V"])
+    cop = np.zeros((9, 9), complex)
+    for b in range(3):
+        cop[3 + b, 6 + b] = np.sqrt(c1["gamma"])                  # |1><r| (x) I
+    kets = np.zeros((4, 9), complex)
+    for k, idx in enumerate((0, 1, 3, 4)):
+        kets[k, idx] = 1.0
+    Hs = np.broadcast_to(np.stack([H1, H2])[None], (4, 2, 9, 9))
+    Ts = np.full((4, 2), c1["tau"])
+    for _ in range(3):
+        SIM.evolve_state_batch(Hs, kets, Ts, [[cop]] * 4, devices=[dev])
+    gen_ms = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        SIM.evolve_state_batch(Hs, kets, Ts, [[cop]] * 4, devices=[dev])
+        gen_ms.append((time.perf_counter() - t0) * 1e3)
     dropin = {k: med([p[k] for p in parts]) for k in ("derive_ms", "engine_ms", "epilogue_ms", "total_ms")}
     dropin["simulate_CZ_gate_ms"] = med(dt)
     dropin["result_assembly_ms"] = med(dt) - dropin["total_ms"]
@@ -353,6 +386,10 @@ def run_c1(args, ws, rank, local, pg):
                         "avg_fidelity": avg_f, "status": st,
                         "note": "host-buffer ryd_run_batch (pack, H2D, kernel, D2H) + ryd_mixed_phase with the "
                                 "16-probe gauge check"},
+        "generic_evolve_state": {"ms": med(gen_ms),
+                                 "note": "simulation.evolve_state_batch (ryd_evolve_generic): the C1 point as dense "
+                                         "9x9 H1, H2 and one jump operator, 4 basis inputs x 2 segments, host arrays in "
+                                         "and out (the reference's evolve_state seam, RG/simulation.py:647-690)"},
         "dropin_default_lp": dict(dropin, note="simulate_CZ_gate(LPSimulationInputs(), include_noise=True): the "
                                                "reference's default noisy LP point (14 c_ops collapsed to 8 channels); "
                                                "breakdown from simulate_CZ_gate_batch(n=1) timings"),
