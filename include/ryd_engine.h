@@ -371,7 +371,8 @@ int ryd_lapack_pool(void* ref_zheevr, const char* path, const char* zheevr_symbo
  * dim <= 16, n_ops <= 32, at most 1024 nonzero operator entries per problem.  Exact
  * propagation per segment (Chebyshev series of exp(dt L), tail < 1e-17) on the handle's
  * first device; host buffers, blocking.  status[i]: RYD_STATUS_STEP_CAP (omega dt above
- * 2e6 rad in one segment; the state is the last one reached), RYD_STATUS_NONFINITE. */
+ * 2e6 rad, or more than 2e5 series terms, in one segment -- mesolve's nsteps cap; the state
+ * is the last one reached), RYD_STATUS_NONFINITE. */
 int ryd_evolve_generic(ryd_handle* h, int dim, int n_seg, int n_ops, int64_t n, int ket,
                        const double* H, const double* dt, const double* ops,
                        const double* state0, double* state_out, uint32_t* status);
