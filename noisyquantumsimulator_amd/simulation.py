@@ -85,8 +85,12 @@ def compute_state_fidelity(psi_out: np.ndarray, psi_target: np.ndarray) -> float
 
 
 def compute_CZ_fidelity(results: Dict[str, np.ndarray], extract_global_phase: bool = True,
-                        hilbert_space_dim: int = 3, eigh=None) -> Tuple[Dict[str, float], float, Dict]:
-    """Per-state fidelities, average and phase_info, as RG/simulation.py:225-633."""
+                        hilbert_space_dim: int = 3, eigh=None,
+                        phases: Optional[Dict[str, float]] = None) -> Tuple[Dict[str, float], float, Dict]:
+    """Per-state fidelities, average and phase_info, as RG/simulation.py:225-633.
+    ``phases`` (mixed states): the dominant-eigenvector phases when they are already known
+    (ryd_mixed_phase computes them with scipy's own zheevr, bit for bit the values eigh
+    would give here), so the four eigendecompositions are not repeated."""
     d = hilbert_space_dim
     idx = {lab: int(np.argmax(np.abs(v))) for lab, v in OPS.basis_kets(d).items()}
     mixed = np.ndim(results["01"]) == 2
@@ -96,14 +100,17 @@ def compute_CZ_fidelity(results: Dict[str, np.ndarray], extract_global_phase: bo
         pops = {lab: float(np.real(results[lab][idx[lab], idx[lab]])) for lab in LABELS}
         fid.update(pops)
         if extract_global_phase:
-            eg = _eigh_fn(eigh)
             ph = {}
-            for lab in LABELS:
-                try:
-                    w, U = eg(results[lab])
-                    ph[lab] = float(np.angle(U[idx[lab], int(np.argmax(w))]))
-                except Exception:
-                    ph[lab] = 0.0
+            if phases is not None:
+                ph = {lab: float(phases[lab]) for lab in LABELS}
+            else:
+                eg = _eigh_fn(eigh)
+                for lab in LABELS:
+                    try:
+                        w, U = eg(results[lab])
+                        ph[lab] = float(np.angle(U[idx[lab], int(np.argmax(w))]))
+                    except Exception:
+                        ph[lab] = 0.0
             cp = float(_wrap(ph["11"] - ph["01"] - ph["10"] + ph["00"]))
             err, pen = _penalty(cp)
             phase_info = {
@@ -286,6 +293,9 @@ class BatchResult:
     process_fidelity: Optional[np.ndarray] = None
     avg_gate_fidelity: Optional[np.ndarray] = None
     timings: Dict[str, float] = field(default_factory=dict)   # host wall ms per stage
+    # (n, 4) dominant-eigenvector phases of the mixed points' rho_00..rho_11 as the reference
+    # forms them (ryd_mixed_phase with scipy's zheevr; NaN for kets and host-eigh runs)
+    phases: Optional[np.ndarray] = None
 
     @property
     def n(self):
@@ -425,6 +435,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     pen = np.ones(nn)
     fpro = np.full(nn, np.nan)
     fgate = np.full(nn, np.nan)
+    phases = np.full((nn, 4), np.nan)
     status = b.status_bits.copy() if b.status_bits is not None else np.zeros(nn, np.uint32)
     states = None
     if return_states:
@@ -464,6 +475,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                 ph, gflags = E.mixed_phase(r.state, idx.size, dim, gauge_check=gauge_check,
                                            copies=gauge_copies if gauge_copies is not None else BATCH_GAUGE_COPIES)
                 cp[idx], pen[idx] = _cp_penalty(ph)
+                phases[idx] = ph
                 status[idx] |= gflags
             need_rho = return_states or host_eigh
             if need_rho:
@@ -487,7 +499,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     return BatchResult(batch=b, avg_fidelity=avg, fidelities=fids, populations=pops,
                        controlled_phase=cp, cz_phase_fidelity=pen, status=status,
                        is_mixed=~ket_mask, states=out_states, kernel_ms=kms, timings=timings,
-                       process_fidelity=fpro, avg_gate_fidelity=fgate)
+                       process_fidelity=fpro, avg_gate_fidelity=fgate, phases=phases)
 
 
 def noise_breakdown_row(b: PH.DerivedBatch, i: int, n_collapse_ops: Optional[int] = None) -> Dict[str, Any]:
@@ -556,7 +568,10 @@ def simulate_CZ_gate(
     mixed = bool(br.is_mixed[0])
     st = br.states["rho" if mixed else "ket"][0]
     results = {lab: st[k] for k, lab in enumerate(LABELS)}
-    fidelities, avg, phase_info = compute_CZ_fidelity(results, True, hilbert_space_dim, eigh=eigh)
+    known = None
+    if mixed and br.phases is not None and np.all(np.isfinite(br.phases[0])):
+        known = dict(zip(LABELS, br.phases[0]))        # the epilogue's scipy-zheevr phases
+    fidelities, avg, phase_info = compute_CZ_fidelity(results, True, hilbert_space_dim, eigh=eigh, phases=known)
     protocol = b.protocol
     is_lp = protocol == "levine_pichler"
     d1 = c["delta_zeeman"] + (c["delta_stark"] if trap_laser_on else 0.0)
