@@ -2572,7 +2572,7 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
     int ns = d->n_steps, sh = d->shape;
     void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
                     (void*)&ldm, (void*)&dstat, (void*)&ns, (void*)&sh};
-    HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(BLOCK), args, 0, stream));
+    HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(D4_BLOCK), args, 0, stream));
     return RYD_OK;
   }
   if (use_sym16(d)) {
@@ -2616,7 +2616,7 @@ int launch_coherences_proto(const double* dp, int64_t n, int64_t ldp, double* dc
     const int64_t blocks = (n + CP_NR - 1) / CP_NR;
     if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
     void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&dc, (void*)&ldc, (void*)&dstat, (void*)&ns, (void*)&sh};
-    HIPCHK(hipLaunchKernel((const void*)coherence_prop_kernel<PROTO>, dim3((unsigned)blocks), dim3(BLOCK), args, 0,
+    HIPCHK(hipLaunchKernel((const void*)coherence_prop_kernel<PROTO>, dim3((unsigned)blocks), dim3(CP_BLOCK), args, 0,
                            stream));
     return RYD_OK;
   }
