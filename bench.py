@@ -241,8 +241,8 @@ def pipelined_c2(params, protocol, n_steps, args, dev, n):
 
 def end_to_end_c2():
     """simulate_CZ_gate_batch on the C2 grid: derivation (host) + engine (host-buffer
-    boundary) + the reference-penalty epilogue (zheevr on host threads, 16-probe gauge
-    check) -- the whole Python drop-in call, wall clock, second of two calls."""
+    boundary) + the reference-penalty epilogue (zheevr on host threads, the batch call's
+    default gauge check) -- the whole Python drop-in call, wall clock, second of two calls."""
     from noisyquantumsimulator_amd import simulation as S
     from noisyquantumsimulator_amd import sweeps as SW
     si, n, kw = SW.omega_delta_call()

@@ -330,8 +330,9 @@ int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* de
  * bit).  `state` = Lindblad sector rows as ryd_run_batch writes them ([25 | 36][ld]).
  * Gauge check: the same procedure on up to n_perturb copies of each rho with the real
  * and imaginary parts of every lower-triangle entry scaled independently by (1 +-
- * rel_eps) (deterministic sign patterns); out_flags[i] |= RYD_STATUS_GAUGE_UNSTABLE as
- * soon as a penalty moves by more than tol.  Host only, n_threads worker threads (0 = all cores). */
+ * rel_eps) (deterministic sign patterns), probed one rho at a time (|11> first; one
+ * zheevr call per probe); out_flags[i] |= RYD_STATUS_GAUGE_UNSTABLE as soon as a
+ * penalty moves by more than tol.  Host only, n_threads worker threads (0 = all cores). */
 #define RYD_MP_V0       0   /* <x|v_max> as (re, im) row pairs, x = 00, 01, 10, 11; the
                                phase is its angle (taken by the caller: the reference
                                uses np.angle)                                       */
