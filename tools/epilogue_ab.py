@@ -1,8 +1,11 @@
 """CPU timing of the host epilogue (ryd_mixed_phase) with and without the gauge check on
 4000 noisy-fixture-derived points (8 threads); compare builds with RYD_ENGINE_LIB=<lib>."""
-import sys, time, os
-_R = __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__)))
-sys.path.insert(0, _R); sys.path.insert(0, _R + '/tests')
+import os
+import sys
+import time
+
+_R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [_R, os.path.join(_R, "tests")]
 import numpy as np
 from test_mixed_phase_host import _noisy_fixture_states
 from noisyquantumsimulator_amd import engine as E
