@@ -197,3 +197,61 @@ def test_lapack_pool_loads_once_per_process():
                                   b"scipy_openblas_set_num_threads", 16, ctypes.byref(got))
     assert got.value == first and (rc == 0) == (first >= 2)   # library cache: same outcome
     assert first <= 8
+
+
+def _splitmix64(x):
+    M = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & M
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+    return x ^ (x >> 31)
+
+
+def _probe_copy(rho, c, x, eps=1e-12):
+    """Copy c of rho_x as ryd_mixed_phase builds it (lower triangle scaled, real and imaginary
+    parts independently; copy 1 all +, copy 2 all -, then splitmix64 signs of (c, x, entry))."""
+    D = rho.shape[0]
+    q = rho.copy()
+    for col in range(D):
+        for row in range(col, D):
+            e = 2 * (row + D * col)
+            h = _splitmix64((c << 32) ^ (x << 24) ^ e)
+            s1 = 1.0 if c == 1 else (-1.0 if c == 2 else (1.0 if h & 1 else -1.0))
+            s2 = 1.0 if c == 1 else (-1.0 if c == 2 else (1.0 if h & 2 else -1.0))
+            q[row, col] = complex(rho[row, col].real * (1.0 + s1 * eps), rho[row, col].imag * (1.0 + s2 * eps))
+    return np.tril(q) + np.tril(q, -1).conj().T
+
+
+def test_gauge_probes_one_rho_at_a_time_match_restatement():
+    """The host gauge check probes copy c of one rho_x at a time, the other three
+    unperturbed: its flag equals a Python restatement of that scheme on scipy.linalg.eigh
+    (any probe that moves the reference penalty by more than 1e-9)."""
+    rng = np.random.default_rng(4)
+    blocks = [S for _, S in _noisy_fixture_states()]
+    n, copies = 27, 3
+    st = np.zeros((25, 4 * n))
+    for i in range(n):
+        S = blocks[i % len(blocks)]
+        scale = 1.0 if i < len(blocks) else (1.0 + 1e-7 * rng.standard_normal(S.shape))
+        st[:, 4 * i:4 * i + 4] = S * scale * (np.abs(S) > 1e-15)
+    ph, flags = E.mixed_phase(st, n, 3, gauge_check=True, copies=copies)
+
+    def phase(rho, x):
+        w, U = sla.eigh(rho)
+        return np.angle(U[IDX[x], int(np.argmax(w))])
+
+    n_flag = 0
+    for i in range(n):
+        rhos = [expand_like_host(st[:, 4 * i + x]) for x in range(4)]
+        p0 = np.array([phase(rhos[x], x) for x in range(4)])
+        assert np.array_equal(p0, ph[i])
+        _, pen0 = SIM._cp_penalty(p0[None])
+        moved = False
+        for x in (3, 0, 1, 2):
+            for c in range(1, copies + 1):
+                p = p0.copy()
+                p[x] = phase(_probe_copy(rhos[x], c, x), x)
+                moved |= abs(SIM._cp_penalty(p[None])[1][0] - pen0[0]) > 1e-9
+        assert bool(flags[i] & N.STATUS_GAUGE_UNSTABLE) == moved, i
+        n_flag += moved
+    assert n_flag > 0                                  # the test exercises flagged points
