@@ -769,6 +769,9 @@ def main():
     ap.add_argument("--c5-shards", type=int, default=0,
                     help="C5: time rank --c5-rank's shard of an N-way split on this one GPU (0: off)")
     ap.add_argument("--c5-rank", type=int, default=0)
+    ap.add_argument("--c4-shards", type=int, default=0,
+                    help="C4: time rank --c4-rank's shard of an N-way split on this one GPU (0: off)")
+    ap.add_argument("--c4-rank", type=int, default=0)
     ap.add_argument("--c5-order", default="omega", choices=["omega", "blocked", "balanced"],
                     help="C5 grid point order (sweeps.blockade_grid_3atom)")
     ap.add_argument("--ladder", type=int, default=-1,
@@ -806,7 +809,10 @@ def main():
                     "reference segments, medium apparatus, 4 collapse ops (sqrt(gamma_r)|1><r| and "
                     "sqrt(gamma_phi) P_r per atom, gamma_r = 1/140 us, gamma_phi = 2pi x 10 kHz)")
     else:
-        batch = SW.c4_rank_shard(rank, ws)
+        # with --c4-shards: one rank's shard of an N-way split on this one GPU (the 1-GPU
+        # strong-scaling proxy, as --c5-shards)
+        batch = (SW.c4_rank_shard(args.c4_rank, args.c4_shards) if args.c4_shards
+                 else SW.c4_rank_shard(rank, ws))
         protocol, n_steps, n_seg = "lp_square", None, 2
         workload = ("C4: 1M-point species {Rb87, Cs133} x T logspace(1-100 uK, 1000) x P_tweezer "
                     "logspace(1-100 mW, 500) LP-square grid, range-sharded over the ranks, "
@@ -898,7 +904,8 @@ def main():
         out_e2e = end_to_end_c2()
         pipelined = pipelined_c2(params, protocol, n_steps, args, dev, n)
     strong = args.workload == "c4"
-    global_points = SW.C4_POINTS if strong else n * ws
+    proxy = strong and args.c4_shards > 0
+    global_points = n if proxy else (SW.C4_POINTS if strong else n * ws)
     total_points = global_points * args.steps
     value = total_points / dt_max
     out = {
@@ -909,6 +916,8 @@ def main():
         "data": "synthetic",
         "config": {"workload": workload, "points_per_gpu": n, "global_points": global_points,
                    "parallelism": f"range-shard x{ws}", "placement": _placement(ws, local, dev),
+                   "shard": (f"rank {args.c4_rank} of {args.c4_shards} (1-GPU strong-scaling proxy: value "
+                             f"counts this shard's points only)" if proxy else None),
                    "method": args.method + ((" (auto: 16-lane DPP-row propagator kernel, phase frame)"
                                              if sym16 else " (auto: propagator kernel, phase frame)")
                                             if args.method == "chebyshev" else "")},

@@ -328,11 +328,14 @@ int ryd_run_trajectories_device(ryd_handle* h, int slot, const ryd_traj_desc* de
  * pi| (:444-452).  Output: the component <x|v_max> per input (the phase is its angle).  `zheevr` is the caller's LAPACK zheevr (Fortran ABI, 32-bit ints;
  * the Python layer passes scipy's, so the phases equal scipy.linalg.eigh's bit for
  * bit).  `state` = Lindblad sector rows as ryd_run_batch writes them ([25 | 36][ld]).
- * Gauge check: the same procedure on up to n_perturb copies of each rho with the real
- * and imaginary parts of every lower-triangle entry scaled independently by (1 +-
- * rel_eps) (deterministic sign patterns), probed one rho at a time (|11> first; one
- * zheevr call per probe); out_flags[i] |= RYD_STATUS_GAUGE_UNSTABLE as soon as a
- * penalty moves by more than tol.  Host only, n_threads worker threads (0 = all cores). */
+ * Gauge check (round 4 semantics): probe (x, c) replaces rho_x alone by copy c of it,
+ * the real and imaginary parts of every lower-triangle entry scaled independently by
+ * (1 +- rel_eps) (copy 1 all +, copy 2 all -, then splitmix64 sign patterns), the other
+ * three rho unperturbed; rho_11 first, then rho_00, rho_01, rho_10, c = 1..n_perturb
+ * each (one zheevr call per probe); out_flags[i] |= RYD_STATUS_GAUGE_UNSTABLE at the
+ * first probe whose penalty moves by more than tol.  Rounds 1-3 perturbed all four rho
+ * together; a flip that needs two phases to move together is not probed any more.  The
+ * oracle's gauge_unstable (scheme "one_rho") is this procedure on scipy.linalg.eigh.  Host only, n_threads worker threads (0 = all cores). */
 #define RYD_MP_V0       0   /* <x|v_max> as (re, im) row pairs, x = 00, 01, 10, 11; the
                                phase is its angle (taken by the caller: the reference
                                uses np.angle)                                       */

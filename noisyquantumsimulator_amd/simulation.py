@@ -349,6 +349,8 @@ def evolve_state(H, psi0, tlist, c_ops=None, options=None, *, devices=None) -> n
     del options
     Hm = _as_array(H)
     v = _as_array(psi0)
+    if v.ndim == 2 and v.shape != Hm.shape[-2:] and 1 in v.shape:
+        v = v.ravel()                       # a Qobj ket's .full() is a (d, 1) column
     tl = np.asarray(tlist, dtype=np.float64)
     T = float(tl[-1] - tl[0]) if tl.size else 0.0
     ops = [_as_array(c) for c in (c_ops or [])]
@@ -361,7 +363,9 @@ def evolve_state_batch(H, psi0, T, c_ops=None, *, devices=None) -> np.ndarray:
     psi0 (n, d) kets or (n, d, d) density matrices; c_ops None or (n, K, d, d) (or a list of
     per-problem lists of K operators).  Kets with c_ops are evolved as |psi><psi|.  Raises
     EngineError for a failed problem (step cap: omega * dt > 2e6 rad in one segment;
-    non-finite)."""
+    non-finite) and ValueError for inputs mesolve would not evolve as given: a segment
+    length that is negative or not finite, a Hamiltonian that is not Hermitian (to 1e-12
+    of its largest entry), column kets (n, d, 1) are taken as kets."""
     from ._native import EngineError, STATUS_FAIL_MASK
     H = np.asarray(H, dtype=np.complex128)
     if H.ndim == 3:
@@ -370,7 +374,15 @@ def evolve_state_batch(H, psi0, T, c_ops=None, *, devices=None) -> np.ndarray:
     T = np.asarray(T, dtype=np.float64).reshape(n, -1)
     if T.shape[1] != n_seg:
         raise ValueError("T must hold one length per segment")
+    if not np.all(np.isfinite(T)) or np.any(T < 0):
+        raise ValueError("segment lengths must be finite and non-negative")
+    scale = np.abs(H).max(axis=(2, 3), initial=0.0)
+    if not np.all(np.isfinite(H)) or np.any(np.abs(H - np.conj(np.swapaxes(H, 2, 3))).max(axis=(2, 3), initial=0.0)
+                                            > 1e-12 * scale):
+        raise ValueError("H must be finite and Hermitian")
     v = np.asarray(psi0, dtype=np.complex128)
+    if v.ndim == 3 and v.shape[1:] in ((d, 1), (1, d)) and d > 1:
+        v = v.reshape(n, d)
     ops = None
     if c_ops is not None and len(c_ops) > 0:
         ops = np.asarray(c_ops, dtype=np.complex128)
@@ -387,10 +399,12 @@ def evolve_state_batch(H, psi0, T, c_ops=None, *, devices=None) -> np.ndarray:
     return out
 
 
-# gauge-check probes of the batch API (round 4: 4, as the optimiser and sweep drivers; was
-# engine.GAUGE_COPIES = 16).  A flagged point usually stops at the first probe; 4 probes miss an
-# unstable point with probability ~50-70 %, 16 with ~10-30 %, 64 with < 1 % --
-# ask for more with gauge_copies when the flag itself is the result being studied.
+# gauge-check probes of the batch API, counted PER RHO (round 4 scheme: probe (x, c) perturbs
+# rho_x alone, rho_11 first, so `copies` = 4 means up to 16 zheevr calls per point, and an
+# unstable point stops at its first moving probe); the optimiser and sweep drivers use the
+# same 4, direct engine.mixed_phase calls engine.GAUGE_COPIES.  Miss rates per probe count
+# under this scheme: DESIGN.md §5 (tools/gauge_miss_rate.py).  Ask for more with
+# gauge_copies when the flag itself is the result being studied.
 BATCH_GAUGE_COPIES = 4
 
 

@@ -204,7 +204,9 @@ def blockade_grid_3atom(n_omega: int = 64, n_vo: int = 64, include_noise: bool =
     vo = np.logspace(1, 3, n_vo)
     if order not in ("blocked", "balanced", "omega"):
         raise ValueError("order must be 'omega', 'blocked' or 'balanced'")
-    if order == "blocked" and n_vo % 8 == 0:
+    if order == "blocked" and n_vo % 8 != 0:
+        raise ValueError("order='blocked' needs n_vo divisible by 8 (8 blocks of V/Omega rows)")
+    if order == "blocked":
         # [block][Omega][V/Omega within the block]
         VB = vo.reshape(8, n_vo // 8)
         OM = np.broadcast_to(om[None, :, None], (8, n_omega, n_vo // 8))

@@ -426,19 +426,66 @@ def snap_structural_zeros(rho: np.ndarray, dim: int = 3) -> np.ndarray:
     return out
 
 
+def _splitmix64(x: int) -> int:
+    M = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & M
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+    return x ^ (x >> 31)
+
+
+def probe_copy(rho: np.ndarray, c: int, x: int, rel_eps: float = 1e-12) -> np.ndarray:
+    """Copy c (1-based) of rho_x as the engine's gauge check builds it: every entry of the
+    lower triangle (what LAPACK reads) with its real and imaginary parts scaled
+    independently by (1 +- rel_eps); copy 1 all +, copy 2 all -, then the signs of
+    splitmix64((c << 32) ^ (x << 24) ^ e), e = 2 (row + D col) (bits 0 / 1)."""
+    D = rho.shape[0]
+    q = rho.copy()
+    for col in range(D):
+        for row in range(col, D):
+            e = 2 * (row + D * col)
+            h = _splitmix64((c << 32) ^ (x << 24) ^ e)
+            s1 = 1.0 if c == 1 else (-1.0 if c == 2 else (1.0 if h & 1 else -1.0))
+            s2 = 1.0 if c == 1 else (-1.0 if c == 2 else (1.0 if h & 2 else -1.0))
+            q[row, col] = complex(rho[row, col].real * (1.0 + s1 * rel_eps),
+                                  rho[row, col].imag * (1.0 + s2 * rel_eps))
+    return np.tril(q) + np.tril(q, -1).conj().T
+
+
 def gauge_unstable(results: Dict[str, np.ndarray], dim: int = 3, rel_eps: float = 1e-12,
-                   copies: int = 64, tol: float = 1e-9, seed: int = 7) -> Tuple[bool, float]:
+                   copies: int = 64, tol: float = 1e-9, seed: int = 7,
+                   scheme: str = "one_rho") -> Tuple[bool, float]:
     """Does the reference's mixed-state penalty (cz_fidelity with scipy.linalg.eigh, the
-    eigensolver QuTiP 5 uses) stay put when the real and imaginary parts of every entry
-    of each rho's lower triangle (what LAPACK reads) are scaled independently by
-    (1 +- rel_eps)?  Copy 1 all +, copy 2 all -, then random sign patterns.  Returns
-    (unstable, max |penalty change|).  The LAPACK eigenvector phase is decided by
-    rounding in the Householder reduction and the tridiagonal eigenvector
-    normalisation, so for most noisy points it is not."""
+    eigensolver QuTiP 5 uses) stay put when the real and imaginary parts of the entries
+    of rho's lower triangle (what LAPACK reads) are scaled independently by (1 +- rel_eps)?
+    Returns (unstable, max |penalty change| over the probes made).  The LAPACK eigenvector
+    phase is decided by rounding in the Householder reduction and the tridiagonal
+    eigenvector normalisation, so for most noisy points it is not.
+
+    scheme "one_rho" (the engine's ryd_mixed_phase, round 4): probe (x, c) perturbs copy c
+    of rho_x alone (probe_copy) with the other three rho unperturbed; rho_11 first, then
+    rho_00, rho_01, rho_10, copies 1..copies each; stops at the first probe that moves the
+    penalty by more than tol.  scheme "all_at_once" (rounds 1-3; how
+    tests/golden/evolution_golden.json's flags were made): copy c perturbs all four rho
+    together, copy 1 all +, copy 2 all -, then numpy sign patterns from ``seed``."""
     eigh = lambda m: sla.eigh(m)
     _, _, info0 = cz_fidelity(results, dim, eigh=eigh)
-    rng = np.random.default_rng(seed)
+    pen0 = info0["cz_phase_fidelity"]
     spread = 0.0
+    if scheme == "one_rho":
+        labs = list(LABELS)
+        for x in (3, 0, 1, 2):
+            for c in range(1, copies + 1):
+                pert = dict(results)
+                pert[labs[x]] = probe_copy(results[labs[x]], c, x, rel_eps)
+                _, _, info = cz_fidelity(pert, dim, eigh=eigh)
+                spread = max(spread, abs(info["cz_phase_fidelity"] - pen0))
+                if spread > tol:
+                    return True, spread
+        return False, spread
+    if scheme != "all_at_once":
+        raise ValueError(f"unknown scheme {scheme!r}")
+    rng = np.random.default_rng(seed)
     for c in range(copies):
         pert = {}
         for lab, rho in results.items():
@@ -451,7 +498,7 @@ def gauge_unstable(results: Dict[str, np.ndarray], dim: int = 3, rel_eps: float 
             q = rho.real * (1.0 + rel_eps * s1) + 1j * rho.imag * (1.0 + rel_eps * s2)
             pert[lab] = np.tril(q) + np.tril(q, -1).conj().T
         _, _, info = cz_fidelity(pert, dim, eigh=eigh)
-        spread = max(spread, abs(info["cz_phase_fidelity"] - info0["cz_phase_fidelity"]))
+        spread = max(spread, abs(info["cz_phase_fidelity"] - pen0))
     return spread > tol, spread
 
 

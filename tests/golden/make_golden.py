@@ -348,7 +348,7 @@ def main():
             # QuTiP keeps the structural zeros exact; the reference's eigensolver is
             # scipy.linalg.eigh (QuTiP 5 Qobj.eigenstates)
             res = {k: O.snap_structural_zeros(v, cfg.get("dim", 3)) for k, v in res.items()}
-            unstable, spread = O.gauge_unstable(res, cfg.get("dim", 3))
+            unstable, spread = O.gauge_unstable(res, cfg.get("dim", 3), scheme="all_at_once")
         import scipy.linalg as sla
         fid, avg, info = O.cz_fidelity(res, eigh=lambda m: sla.eigh(m))
         states = {k: (np.stack([v.real, v.imag]).tolist()) for k, v in res.items()}

@@ -105,3 +105,25 @@ def test_step_cap_is_a_failure():
     c, H1, _, cop = _c1()
     with pytest.raises(N.EngineError):
         SIM.evolve_state(H1, O.initial_kets(3)["11"], [0.0, 1.0], cop)      # omega T ~ 1e10 rad
+
+
+@pytest.mark.parametrize("with_cops", [False, True])
+def test_column_ket_like_a_qobj(with_cops):
+    """A Qobj ket's .full() is a (d, 1) column: evolve_state takes it as the ket the
+    reference's mesolve call passes (RG/simulation.py:649), with and without c_ops."""
+    c, H1, _, cop = _c1()
+    psi = O.initial_kets(3)["11"]
+
+    class _Q:                                 # the one Qobj method evolve_state reads
+        def __init__(self, a):
+            self.a = a
+
+        def full(self):
+            return self.a
+    ops = [_Q(cop[0])] if with_cops else None
+    col = SIM.evolve_state(_Q(H1), _Q(psi[:, None]), [0.0, c["tau"]], ops)
+    flat = SIM.evolve_state(H1, psi, [0.0, c["tau"]], cop if with_cops else None)
+    np.testing.assert_array_equal(col, flat)
+    assert col.shape == ((9, 9) if with_cops else (9,))
+    ref = O.evolve_state(H1, psi, [0.0, c["tau"]], cop if with_cops else ())
+    assert np.max(np.abs(col - ref)) < TOL

@@ -32,7 +32,8 @@ def test_temperature_sweep_against_oracle():
             assert T[i] == pytest.approx(b["tau_total"][0] * 1e6, rel=1e-12)
             assert VO[i] == pytest.approx(b["V_over_Omega"][0], rel=1e-12)
             res = {k: O.snap_structural_zeros(v) for k, v in O.run_point(point_spec(b, 0)).items()}
-            unstable, _ = O.gauge_unstable(res)
+            # the engine's one-rho-at-a-time probes with the sweep's probe count
+            unstable, _ = O.gauge_unstable(res, copies=RS.SWEEP_GAUGE_COPIES)
             fid, avg, info = O.cz_fidelity(res, eigh=lambda m: sla.eigh(m))
             assert bool(ST[i] & N.STATUS_GAUGE_UNSTABLE) == unstable, (proto, t)
             if not unstable:

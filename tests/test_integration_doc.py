@@ -1,10 +1,13 @@
 """INTEGRATION.md is executable: the Option A import block runs against the package,
-and the Option B ctypes stub binds the in-tree libryd_engine.so (symbols and struct
-layout; no compute -- ryd_create just reports that this container has no GPU)."""
+and the Option B ctypes stub binds the in-tree libryd_engine.so (symbols, struct layout
+and the ABI version taken from the library on CPU; on the GPU the stub's lp_square_rho
+runs SURVEY §8(d)'s C1 point and is compared with the oracle -- the two mesolve calls of
+RG/simulation.py:740-776 restated with expm -- at 1e-10)."""
 import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 from noisyquantumsimulator_amd import _native as N
@@ -30,16 +33,53 @@ def test_option_a_import_block():
         assert hasattr(pkg, name), name
 
 
-def test_option_b_stub_binds_the_library():
+def _exec_stub():
     if not os.path.exists(N.LIB_PATH):
         pytest.skip("libryd_engine.so not built")
     stub = next(b for b in _blocks() if "ctypes stub" in b)
     stub = stub.replace('ctypes.CDLL("libryd_engine.so")', f'ctypes.CDLL({N.LIB_PATH!r})')
     ns = {}
     exec(compile(stub, "INTEGRATION.md:option-B", "exec"), ns)
+    return stub, ns
+
+
+def test_option_b_stub_binds_the_library():
+    stub, ns = _exec_stub()
+    # the descriptor's abi_version comes from the library, never from a literal
+    assert "_Desc(_ABI," in stub
+    assert not re.search(r"_Desc\(\s*\d", stub)
+    assert not re.search(r"ABI\s+\d", stub)
+    assert ns["_ABI"] == N.RYD_ABI_VERSION
     assert ctypes.sizeof(ns["_Desc"]) == ctypes.sizeof(N.BatchDesc)
     for (fa, ta), (fb, tb) in zip(ns["_Desc"]._fields_, N.BatchDesc._fields_):
         assert fa == fb and ctypes.sizeof(ta) == ctypes.sizeof(tb)
         assert getattr(ns["_Desc"], fa).offset == getattr(N.BatchDesc, fb).offset
     assert callable(ns["lp_square_rho"])
     assert ns["_lib"].ryd_abi_version() == N.RYD_ABI_VERSION
+
+
+@pytest.mark.gpu
+def test_option_b_stub_runs_c1_point_against_oracle():
+    """The stub a maintainer pastes into RG/ (replacing evolve_two_pulse_lp's 8 mesolve
+    calls) on the C1 point (one collapse operator sqrt(gamma)|1><r| on atom A only, so
+    the unequal-atom rate columns): its 25 sector coordinates per input, expanded with
+    engine.expand_rho, equal the oracle's rho (H1 then H2 = H(Omega xi), expm) at 1e-10
+    and the package engine's rows bit for bit."""
+    from noisyquantumsimulator_amd import engine as E
+    from noisyquantumsimulator_amd import simulation as SIM
+    from noisyquantumsimulator_amd import sweeps as SW
+    from oracle import lindblad_oracle as O
+    _, ns = _exec_stub()
+    c = SW.c1_point()
+    st, sm, ok = ns["lp_square_rho"](c["Omega"], c["Delta"], c["V"], 0.0, c["tau"], c["xi"],
+                                     (c["gamma"], 0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 0.0))
+    assert ok[0] & N.STATUS_FAIL_MASK == 0
+    rho = E.expand_rho(st, 1, 3)[0]
+    H1 = O.two_atom_hamiltonian(c["Omega"], c["Delta"], c["V"])
+    H2 = O.two_atom_hamiltonian(c["Omega"] * c["xi"], c["Delta"], c["V"])
+    cop = [np.sqrt(c["gamma"]) * O._two(O._trans(3, 1, 2), np.eye(3))]
+    for k, psi in enumerate(O.initial_kets(3).values()):
+        ref = O.evolve_state(H2, O.evolve_state(H1, psi, [0, c["tau"]], cop), [0, c["tau"]], cop)
+        assert np.max(np.abs(rho[k] - ref)) < 1e-10, k
+    r = SIM._engine().run(SW.c1_params(), "lp_square", "lindblad")
+    np.testing.assert_array_equal(st, r.state)

@@ -199,27 +199,7 @@ def test_lapack_pool_loads_once_per_process():
     assert first <= 8
 
 
-def _splitmix64(x):
-    M = (1 << 64) - 1
-    x = (x + 0x9E3779B97F4A7C15) & M
-    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
-    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
-    return x ^ (x >> 31)
-
-
-def _probe_copy(rho, c, x, eps=1e-12):
-    """Copy c of rho_x as ryd_mixed_phase builds it (lower triangle scaled, real and imaginary
-    parts independently; copy 1 all +, copy 2 all -, then splitmix64 signs of (c, x, entry))."""
-    D = rho.shape[0]
-    q = rho.copy()
-    for col in range(D):
-        for row in range(col, D):
-            e = 2 * (row + D * col)
-            h = _splitmix64((c << 32) ^ (x << 24) ^ e)
-            s1 = 1.0 if c == 1 else (-1.0 if c == 2 else (1.0 if h & 1 else -1.0))
-            s2 = 1.0 if c == 1 else (-1.0 if c == 2 else (1.0 if h & 2 else -1.0))
-            q[row, col] = complex(rho[row, col].real * (1.0 + s1 * eps), rho[row, col].imag * (1.0 + s2 * eps))
-    return np.tril(q) + np.tril(q, -1).conj().T
+_probe_copy = O.probe_copy
 
 
 def test_gauge_probes_one_rho_at_a_time_match_restatement():
