@@ -175,12 +175,16 @@ def scipy_zheevr() -> int:
 
 
 _pool_size: Optional[int] = None
-LAPACK_POOL_DEFAULT = 8     # copies (each holds a glibc link namespace; RYD_LAPACK_POOL raises it, C cap 15)
+# copies (each holds a glibc link namespace; RYD_LAPACK_POOL sets it, C cap 15).  Round 5: 11,
+# what loads on the GPU box beside torch before glibc refuses another namespace; a request
+# above what loads keeps the copies that did load (tests/test_mixed_phase_host.py checks
+# that such a partial pool stays bit-identical)
+LAPACK_POOL_DEFAULT = 11
 
 
 def lapack_pool_copies(n_threads: int) -> int:
     """Copies the epilogue asks for: RYD_LAPACK_POOL (0 = off, N = at most N copies),
-    default min(n_threads, 8)."""
+    default min(n_threads, LAPACK_POOL_DEFAULT)."""
     env = os.environ.get("RYD_LAPACK_POOL")
     cap = LAPACK_POOL_DEFAULT
     if env is not None and env.strip() != "":
