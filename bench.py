@@ -516,10 +516,12 @@ FLOP_PER_DIM4_TERM = 2 * 6 * (2 * 16 + 3) + 2 * 16 + 2 * 36
 FLOP_PER_COH_POINT_TERM = 2 * 332 + 2 * 332 + 148 + 144
 # lindblad4_prop_kernel (ryd_dim4_prop.inc): one triangle-generator application (apply_Lsym4:
 # the single-atom rows twice per output, 7 x (3+7+8+7+7+4) = 252 flops, the V term 32, the
-# Clenshaw add 21), one 21 x 21 squaring (9261 FMA), one segment (21^2 + 6^2 FMA + the
-# frames), one 6-vector column term (36 + 12; the 6 x 6 squarings, <= 432 flops each, not counted)
+# Clenshaw add 21) per term of each of the 15 D columns, one 6-vector column term (36 + 12)
+# per term of each of the 6 B columns, one block-triangular squaring (round 5: the useful
+# products only -- D D 15^3, B C + C D 6 x 6 x 15 + 6 x 15^2, B B 6^3 = 5481 FMA), one
+# segment (21^2 + 6^2 FMA + the frames)
 FLOP_PER_D4_APPLY = 252 + 32 + 21
-FLOP_PER_D4_SQUARING = 2 * 21 ** 3
+FLOP_PER_D4_SQUARING = 2 * (15 ** 3 + 6 * 6 * 15 + 6 * 15 ** 2 + 6 ** 3)
 FLOP_PER_D4_SEGMENT = 2 * 21 ** 2 + 4 * 21 + 2 * 6 ** 2 + 8
 FLOP_PER_D4_VEC_TERM = 36 + 12
 
@@ -528,10 +530,12 @@ def coh_prop_flops(params: np.ndarray, protocol: str) -> float:
     """Algorithmic flops of coherence_prop_kernel (ryd_coh_prop.inc) on a batch: per sector
     built (the (0,-1) sector, n = 10; (-1,-1) and (-1,+1), n = 4; (-1,0) too when the atoms
     differ) n Chebyshev columns x the series terms at x / 2^s (332 / 148 / 144 flops per
-    term and column, as coherence_cheb_kernel's applications) + s squarings (n^3 complex
-    MACs) + per segment the inputs' n^2 complex MACs.  The kernel's own omega and s, restated
-    (h_bounds + the rate sum; s = ceil(log2(x / CP_XS)), CP_XS = 2); LP square and smooth JP
-    build once."""
+    term and column, as coherence_cheb_kernel's applications) + s squarings (the useful
+    complex MACs of one squaring: 680 for n = 10, whose 2 invariant columns take 4 products
+    each and the other 8 columns 84; 64 for n = 4) + per segment the inputs' n^2 complex
+    MACs.  The kernel's own omega and s, restated (h_bounds + the rate sum;
+    s = ceil(log2(x / CP_XS)), CP_XS = 0.5, terms = cheb_terms_small + 1); LP square and
+    smooth JP build once."""
     from noisyquantumsimulator_amd import _native as N
     P = N.P
     Om, Dl, V, d1 = params[P["OMEGA"]], params[P["DELTA"]], params[P["V"]], params[P["DELTA1"]]
@@ -548,15 +552,29 @@ def coh_prop_flops(params: np.ndarray, protocol: str) -> float:
             emin, emax = np.minimum(emin, E - r), np.maximum(emax, E + r)
     rsum = np.abs(params[P["G1_A"]:P["GSC_A"] + 1]).sum(0) + np.abs(params[P["G1_B"]:P["GSC_B"] + 1]).sum(0)
     x = (emax - emin + rsum) * dt
-    s = np.where(x > 2.0, np.ceil(np.log2(np.maximum(x, 1e-300) / 2.0)), 0.0)     # CP_XS
+    s = np.where(x > CP_XS, np.ceil(np.log2(np.maximum(x, 1e-300) / CP_XS)), 0.0)
     xs = x / 2.0 ** s
-    terms = np.array([_cheb_terms(v) + 1 for v in xs], float)
+    terms = np.array([_cheb_terms_small(v) + 1 for v in xs], float)
     sym = np.all(params[P["G1_A"]:P["GSC_A"] + 1] == params[P["G1_B"]:P["GSC_B"] + 1], axis=0)
     f = 0.0
-    for n, per_term, nin, on in ((10, 332, 2, np.ones_like(sym)), (10, 332, 2, ~sym), (4, 148, 1, np.ones_like(sym)),
-                                 (4, 144, 1, np.ones_like(sym))):
-        f += float((on * (n * terms * per_term + s * n ** 3 * 8 + nseg * nin * n * n * 8)).sum())
+    for n, per_term, sq_macs, nin, on in ((10, 332, 680, 2, np.ones_like(sym)), (10, 332, 680, 2, ~sym),
+                                          (4, 148, 64, 1, np.ones_like(sym)), (4, 144, 64, 1, np.ones_like(sym))):
+        f += float((on * (n * terms * per_term + s * sq_macs * 8 + nseg * nin * n * n * 8)).sum())
     return f
+
+
+CP_XS = 0.5                      # ryd_coh_prop.inc
+# ryd_sym16.inc cheb_terms_small: the smallest doubles h = x / 2 whose j-th term reaches 1e-17
+_TH_SMALL = (1e-17, 4.4721359549995795e-09, 3.914867641168864e-06, 0.00012446659545769568,
+             0.0010371372893366482, 0.004394290351366487, 0.0125993232817844, 0.02822864716464555,
+             0.05356271212458357, 0.09036001686117834, 0.1398168813097236, 0.20262580209060138,
+             0.2790704614462359, 0.36912378048400807, 0.47253426642798413, 0.5888961629494429,
+             0.7177037357024775)
+
+
+def _cheb_terms_small(x: float) -> int:
+    h = 0.5 * x
+    return 1 + sum(1 for t in _TH_SMALL if h >= t)
 
 
 def _cheb_terms(x: float) -> int:
@@ -655,9 +673,9 @@ def run_aux(args, ws, rank, local, pg):
         elif args.workload == "dim4" and os.environ.get("RYD_DIM4_PROP", "1") != "0":
             kernel = "lindblad4_prop_kernel"           # NMV_USEFUL / NMV_EXEC: terms per triangle / 6-vector column
             nseg = 2
-            flops = (float(res.col("NMV_USEFUL").sum()) * 21 * FLOP_PER_D4_APPLY
+            flops = (float(res.col("NMV_USEFUL").sum()) * (15 * FLOP_PER_D4_APPLY + 6 * FLOP_PER_D4_VEC_TERM)
                      + float(res.col("NSQUARE").sum()) * FLOP_PER_D4_SQUARING
-                     + n * nseg * FLOP_PER_D4_SEGMENT + float(res.col("NMV_EXEC").sum()) * 6 * FLOP_PER_D4_VEC_TERM)
+                     + n * nseg * FLOP_PER_D4_SEGMENT)
         else:
             per = {"shaped": FLOP_PER_MATVEC, "dim4": FLOP_PER_DIM4_TERM, "ket_cheb": FLOP_PER_KET_TERM}[args.workload]
             flops = res.matvec_useful * per
