@@ -85,3 +85,24 @@ def test_simulate_cz_gate_dim4_drop_in():
     r4 = SIM.simulate_CZ_gate(si, hilbert_space_dim=4, include_noise=False, **KW)
     r3 = SIM.simulate_CZ_gate(si, hilbert_space_dim=3, include_noise=False, **KW)
     assert abs(r4.avg_fidelity - r3.avg_fidelity) < 1e-13
+
+
+def test_dim4_rows_are_independent_of_their_wave(eng):
+    """The DPP-row kernel holds 4 points per wave with per-row squaring depths: a ragged
+    batch of 9 points (Omega spread over a decade: different depths in one wave) gives each
+    point the bits it gets alone, and the oracle's states at 1e-10."""
+    warnings.simplefilter("ignore")
+    n = 9
+    b = PH.derive_batch(CF.LPSimulationInputs(excitation=_exc()), n, hilbert_space_dim=4,
+                        **dict(KW, temperature=np.linspace(1e-6, 3e-5, n)),
+                        overrides=dict(laser_2_power=np.geomspace(0.03, 3.0, n)))
+    p = E.pack_params(b)
+    r = eng.run(p, "lp_square", "lindblad", dim=4)
+    assert np.all(r.status == 0)
+    assert len(set(r.col("NSQUARE").tolist())) > 1              # different depths in the batch
+    for i in (0, 4, 8):
+        one = eng.run(p[:, i:i + 1].copy(), "lp_square", "lindblad", dim=4)
+        np.testing.assert_array_equal(one.state[:, :4], r.state[:, 4 * i:4 * i + 4])
+        ref = O.run_point(OE.point_spec(b, i))
+        for k, lab in enumerate(O.LABELS):
+            np.testing.assert_allclose(r.rho()[i, k], ref[lab], atol=TOL, rtol=0, err_msg=f"{i}/{lab}")

@@ -64,3 +64,15 @@ def test_large_batch_channel_properties(eng):
     for i in (0, n - 1):
         ref = O.process_map(spec_from_params(p, i, "lp_square"))
         np.testing.assert_allclose(pm.S[i], ref, atol=TOL, rtol=0)
+
+
+def test_coherence_rows_are_independent_of_their_wave(eng):
+    """4 points per wave, each row (and each quad bank) with its own squaring depth: a
+    ragged batch gives every point the bits it gets alone."""
+    rng = np.random.default_rng(17)
+    p = _random_points(rng, 7, "lp_square")
+    coh, st = eng.run_coherences(p, "lp_square")
+    assert np.all(st == 0)
+    for i in (0, 3, 6):
+        c1, s1 = eng.run_coherences(p[:, i:i + 1].copy(), "lp_square")
+        np.testing.assert_array_equal(c1[:, 0], coh[:, i])
