@@ -521,6 +521,10 @@ FLOP_PER_COH_POINT_TERM = 2 * 332 + 2 * 332 + 148 + 144
 # products only -- D D 15^3, B C + C D 6 x 6 x 15 + 6 x 15^2, B B 6^3 = 5481 FMA), one
 # segment (21^2 + 6^2 FMA + the frames)
 FLOP_PER_D4_APPLY = 252 + 32 + 21
+# lindblad_shaped16_kernel (ryd_shaped16.inc), per series term of a point: the triangle
+# generator (apply_Lsym: 95 FMAs), the single-atom 5-vector (13 FMAs + 2 subtractions) and the
+# Clenshaw update of the 20 coordinates (a_k v + ... + b2: one FMA and one add each)
+FLOP_PER_SHAPED16_TERM = 2 * 95 + 2 * 13 + 2 + 4 * 20
 FLOP_PER_D4_SQUARING = 2 * (15 ** 3 + 6 * 6 * 15 + 6 * 15 ** 2 + 6 ** 3)
 FLOP_PER_D4_SEGMENT = 2 * 21 ** 2 + 4 * 21 + 2 * 6 ** 2 + 8
 FLOP_PER_D4_VEC_TERM = 36 + 12
@@ -633,7 +637,7 @@ def run_aux(args, ws, rank, local, pg):
         db = E.CoherenceDeviceBatch(eng, params, protocol)
     else:
         db = E.DeviceBatch(eng, params, protocol, evolution, n_steps=n_steps, shape=shape,
-                           method="chebyshev" if args.workload == "ket" or dim == 4 else "cheb_vector", dim=dim)
+                           method="chebyshev" if args.workload in ("ket", "shaped") or dim == 4 else "cheb_vector", dim=dim)
     for _ in range(args.warmup):
         db.launch()
     db.synchronize()
@@ -670,6 +674,9 @@ def run_aux(args, ws, rank, local, pg):
         if args.workload == "ket":
             flops = (res.matvec_useful * FLOP_PER_KET_BLOCK_SEG
                      + float(res.col("NSQUARE").sum()) * FLOP_PER_KET_BLOCK_BUILD)
+        elif args.workload == "shaped" and os.environ.get("RYD_SHAPED16", "1") != "0":
+            kernel = "lindblad_shaped16_kernel"        # NMV_USEFUL: series terms per point
+            flops = float(res.col("NMV_USEFUL").sum()) * FLOP_PER_SHAPED16_TERM
         elif args.workload == "dim4" and os.environ.get("RYD_DIM4_PROP", "1") != "0":
             kernel = "lindblad4_prop_kernel"           # NMV_USEFUL / NMV_EXEC: terms per triangle / 6-vector column
             nseg = 2

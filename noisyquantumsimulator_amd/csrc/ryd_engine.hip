@@ -2315,6 +2315,7 @@ __global__ __launch_bounds__(BLOCK) void coherence_cheb_kernel(const double* __r
 
 #include "ryd_coh_prop.inc"
 #include "ryd_dim4_prop.inc"
+#include "ryd_shaped16.inc"
 
 // ---------------------------------------------------------------------------
 // host side
@@ -2359,6 +2360,15 @@ bool use_sym16(const ryd_batch_desc* d) {
          (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0 &&
          (d->protocol == RYD_PROTO_LP_SQUARE || d->protocol == RYD_PROTO_BANGBANG ||
           d->protocol == RYD_PROTO_SMOOTH_JP);
+}
+
+// LP shaped, identical atoms, the auto method: the 16-lane DPP-row state-vector kernel
+// (ryd_shaped16.inc); RYD_SHAPED16=0 keeps lindblad_cheb_kernel (the cross-check)
+bool use_shaped16(const ryd_batch_desc* d) {
+  const char* e = getenv("RYD_SHAPED16");
+  if (e && e[0] == '0') return false;
+  return d->dim == 3 && d->evolution == RYD_EVOL_LINDBLAD && d->method == RYD_METHOD_CHEBYSHEV &&
+         (d->flags & RYD_FLAG_SYMMETRIC_ATOMS) != 0 && d->protocol == RYD_PROTO_LP_SHAPED;
 }
 
 // dim 4, identical atoms, constant-|Omega| schedules: the triangle propagator kernel
@@ -2573,6 +2583,16 @@ int launch(const ryd_batch_desc* d, const double* dp, int64_t n, int64_t ldp, do
     void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
                     (void*)&ldm, (void*)&dstat, (void*)&ns, (void*)&sh};
     HIPCHK(hipLaunchKernel((const void*)f, dim3((unsigned)blocks), dim3(D4_BLOCK), args, 0, stream));
+    return RYD_OK;
+  }
+  if (use_shaped16(d)) {
+    const int64_t blocks = (n + SH_PPW - 1) / SH_PPW;
+    if (blocks > 0x7fffffffLL) return fail(RYD_ERR_INVALID, "batch too large for one launch");
+    int ns = d->n_steps, sh = d->shape;
+    void* args[] = {(void*)&dp, (void*)&n, (void*)&ldp, (void*)&ds, (void*)&lds, (void*)&dm,
+                    (void*)&ldm, (void*)&dstat, (void*)&ns, (void*)&sh};
+    HIPCHK(hipLaunchKernel((const void*)lindblad_shaped16_kernel<RYD_PROTO_LP_SHAPED>, dim3((unsigned)blocks),
+                           dim3(SH_BLOCK), args, 0, stream));
     return RYD_OK;
   }
   if (use_sym16(d)) {
