@@ -42,6 +42,11 @@ if L == 0 and os.environ.get("RYD_T_WG", "0") == "1":      # traj3w_kernel: the 
           f"{(ev.sum() + jf.sum()) / trips.sum():.0f} (restart + evaluation {ev.sum() / trips.sum():.0f}, "
           f"segments/jumps/ends/fetch {jf.sum() / trips.sum():.0f})")
     sys.exit(0)
+if L == 0:                       # traj3e_kernel: the outputs phase's split (range merges)
+    arr, mrg = r.col("ITER_USEFUL"), r.col("ITER_EXEC")
+    print(f"  (of outputs: the merge's jumper lists mean {arr.mean():.0f} p90 {np.percentile(arr, 90):.0f}; "
+          f"merge in all (lists, ket loads, reduction) mean {mrg.mean():.0f} p90 {np.percentile(mrg, 90):.0f})")
+    sys.exit(0)
 use, ex = r.col("ITER_USEFUL"), r.col("ITER_EXEC")
 print(f"  ladder steps useful {use.sum():.3g}, executed {ex.sum():.3g} (exec/useful {ex.sum() / use.sum():.2f}); "
       f"walk cycles per executed wave-step {r.col('MAX_JUMPS').sum() / (ex.sum() / 64):.0f}")
