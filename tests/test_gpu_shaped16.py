@@ -58,3 +58,19 @@ def test_shaped16_rows_independent_of_their_wave(eng):
     for i in (1, 5):
         one = eng.run(p[:, i:i + 1].copy(), "lp_shaped", "lindblad", shape="cosine", n_steps=40)
         np.testing.assert_array_equal(one.state[:, :4], r.state[:, 4 * i:4 * i + 4])
+
+
+@pytest.mark.parametrize("n_steps", [3, 40])
+def test_shaped16_coarse_schedule_substeps(eng, n_steps):
+    """Segments whose series argument exceeds SH_XSUB are taken in equal sub-steps (rows of a
+    wave with different counts): same states as the per-lane kernel, no STEP_CAP."""
+    b = _batch(7)
+    p = E.pack_params(b)
+    r = eng.run(p, "lp_shaped", "lindblad", shape="cosine", n_steps=n_steps)
+    assert np.all(r.status == 0)
+    os.environ["RYD_SHAPED16"] = "0"
+    try:
+        old = eng.run(p, "lp_shaped", "lindblad", shape="cosine", n_steps=n_steps)
+    finally:
+        del os.environ["RYD_SHAPED16"]
+    np.testing.assert_allclose(r.state, old.state, atol=TOL, rtol=0)
