@@ -74,3 +74,20 @@ def test_shaped16_coarse_schedule_substeps(eng, n_steps):
     finally:
         del os.environ["RYD_SHAPED16"]
     np.testing.assert_allclose(r.state, old.state, atol=TOL, rtol=0)
+
+
+@pytest.mark.parametrize("shape,n_steps", [("square", 2), ("blackman", 2), ("cosine", 2), ("blackman", 500)])
+def test_shaped16_every_shape_and_the_shortest_schedule(eng, shape, n_steps):
+    """The four envelope names (square / gaussian / blackman take the scalar-t envelope 1,
+    RG/simulation.py:2179-2220) and n_steps = 2 (one segment per pulse, sub-stepped): the
+    same states as the per-lane kernel."""
+    b = _batch(5)
+    p = E.pack_params(b)
+    r = eng.run(p, "lp_shaped", "lindblad", shape=shape, n_steps=n_steps)
+    assert np.all(r.status == 0)
+    os.environ["RYD_SHAPED16"] = "0"
+    try:
+        old = eng.run(p, "lp_shaped", "lindblad", shape=shape, n_steps=n_steps)
+    finally:
+        del os.environ["RYD_SHAPED16"]
+    np.testing.assert_allclose(r.state, old.state, atol=TOL, rtol=0)
