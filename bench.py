@@ -593,9 +593,10 @@ def _cheb_terms(x: float) -> int:
     return int(np.ceil(x + 12.0 * np.cbrt(x) + 10.0))
 AUX = {
     # name: (kernel, state rows per input (0: coherence), bytes per point, description)
-    "shaped": ("lindblad_cheb_kernel", 25, 8 * 16 + 8 * 100 + 8 * 19 + 4,
+    "shaped": ("lindblad_shaped16_kernel", 25, 8 * 16 + 8 * 100 + 8 * 19 + 4,
                "C2 (Omega, Delta) grid with the cosine-shaped LP pulse (RG/simulation.py:2099-2231: 2 x 499 "
-               "segments of tau/500, envelope sin^2, area correction 2), full reference noise, 25-dim sector"),
+               "segments of tau/500, envelope sin^2, area correction 2), full reference noise, 25-dim sector "
+               "(RYD_SHAPED16=0: lindblad_cheb_kernel, the per-lane Chebyshev cross-check)"),
     "dim4": ("lindblad4_cheb_kernel", 36, 8 * 17 + 8 * 144 + 8 * 19 + 4,
              "C2 (Omega, Delta) grid, LP square, hilbert_space_dim=4 (mJ sublevels r+/r-, mJ mixing; "
              "RG/hamiltonians.py:490-853), full reference noise, 36-dim sector"),
@@ -684,6 +685,8 @@ def run_aux(args, ws, rank, local, pg):
                      + float(res.col("NSQUARE").sum()) * FLOP_PER_D4_SQUARING
                      + n * nseg * FLOP_PER_D4_SEGMENT)
         else:
+            if args.workload == "shaped":
+                kernel = "lindblad_cheb_kernel"            # RYD_SHAPED16=0
             per = {"shaped": FLOP_PER_MATVEC, "dim4": FLOP_PER_DIM4_TERM, "ket_cheb": FLOP_PER_KET_TERM}[args.workload]
             flops = res.matvec_useful * per
         useful_exec = (res.matvec_exec / max(res.matvec_useful, 1.0)

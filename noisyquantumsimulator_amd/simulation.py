@@ -196,8 +196,17 @@ def mixed_phase_penalty(rho: np.ndarray, eigh=None) -> Tuple[np.ndarray, np.ndar
 
 @dataclass
 class SimulationResult:
-    """Same fields and properties as RG/simulation.py:2238-2531.  ``results``,
-    ``H1``, ``H2``, ``c_ops`` are numpy arrays (the reference returns qutip.Qobj)."""
+    """Same fields and properties as RG/simulation.py:2238-2531, with one drop-in
+    difference in the types of four fields: the reference fills ``results`` (label ->
+    final state), ``H1``, ``H2`` and ``c_ops`` with ``qutip.Qobj`` objects
+    (RG/simulation.py:689-690, :3589-3676); here they are numpy ``ndarray``s holding the
+    same matrices -- ``results[label]`` a (D, D) complex128 density matrix (noisy runs)
+    or a (D,) ket (noise-free runs), ``H1``/``H2`` (D, D) complex128, ``c_ops`` a list
+    of (D, D) complex128 -- in the same basis order and QuTiP's dense layout
+    (``Qobj.full()`` of the reference's objects).  qutip is not a dependency of this
+    package; a caller that needs Qobj methods wraps them with ``qutip.Qobj(arr,
+    dims=[[d, d], [d, d]])``.  No caller inside the reference uses Qobj methods on these
+    fields."""
     avg_fidelity: float
     fidelities: Dict[str, float]
     phase_info: Dict
@@ -363,9 +372,12 @@ def evolve_state_batch(H, psi0, T, c_ops=None, *, devices=None) -> np.ndarray:
     psi0 (n, d) kets or (n, d, d) density matrices; c_ops None or (n, K, d, d) (or a list of
     per-problem lists of K operators).  Kets with c_ops are evolved as |psi><psi|.  Raises
     EngineError for a failed problem (step cap: omega * dt > 2e6 rad in one segment;
-    non-finite) and ValueError for inputs mesolve would not evolve as given: a segment
-    length that is negative or not finite, a Hamiltonian that is not Hermitian (to 1e-12
-    of its largest entry), column kets (n, d, 1) are taken as kets."""
+    non-finite) and ValueError for inputs this engine does not evolve: a segment length
+    that is negative or not finite, and a Hamiltonian that is not finite or not Hermitian
+    (to 1e-12 of its largest entry).  The reference's mesolve WOULD evolve a non-Hermitian
+    H through its Liouvillian; this engine does not support it (its Gershgorin series
+    bound assumes a real diagonal), so such inputs are refused rather than evolved
+    inexactly.  Column kets (n, d, 1) are taken as kets."""
     from ._native import EngineError, STATUS_FAIL_MASK
     H = np.asarray(H, dtype=np.complex128)
     if H.ndim == 3:
@@ -379,7 +391,8 @@ def evolve_state_batch(H, psi0, T, c_ops=None, *, devices=None) -> np.ndarray:
     scale = np.abs(H).max(axis=(2, 3), initial=0.0)
     if not np.all(np.isfinite(H)) or np.any(np.abs(H - np.conj(np.swapaxes(H, 2, 3))).max(axis=(2, 3), initial=0.0)
                                             > 1e-12 * scale):
-        raise ValueError("H must be finite and Hermitian")
+        raise ValueError("H must be finite and Hermitian: this engine does not evolve a non-Hermitian H "
+                         "(the reference's mesolve would, through its Liouvillian)")
     v = np.asarray(psi0, dtype=np.complex128)
     if v.ndim == 3 and v.shape[1:] in ((d, 1), (1, d)) and d > 1:
         v = v.reshape(n, d)

@@ -127,3 +127,27 @@ def test_column_ket_like_a_qobj(with_cops):
     assert col.shape == ((9, 9) if with_cops else (9,))
     ref = O.evolve_state(H1, psi, [0.0, c["tau"]], cop if with_cops else ())
     assert np.max(np.abs(col - ref)) < TOL
+
+
+def test_large_batch_host_memory_is_bounded():
+    """the sparse-row path sizes its host tables to the batch's real row width
+    (two passes over the row builder) instead of a 16-wide staging copy beside the upload
+    blob.  8192 copies of the C1 problem (D = 9, rows <= 8 wide): the blob is ~212 MB; the
+    process's peak RSS may not grow by more than twice that.  Every problem's rho equals
+    problem 0's bit for bit, and problem 0 equals the oracle."""
+    import resource
+    c, H1, H2, cop = _c1()
+    n = 8192
+    H = np.broadcast_to(np.stack([H1, H2])[None], (n, 2, 9, 9))
+    T = np.full((n, 2), c["tau"])
+    psi = O.initial_kets(3)["11"]
+    kets = np.broadcast_to(psi[None], (n, 9))
+    ops = np.broadcast_to(np.stack(cop)[None], (n, 1, 9, 9))
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
+    out = SIM.evolve_state_batch(H, kets, T, ops)
+    grew = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024 - rss0
+    blob = n * 2 * 81 * 8 * (16 + 4)
+    assert grew < 2 * blob, (grew, blob)
+    assert np.array_equal(out, np.broadcast_to(out[0], out.shape))
+    ref = O.evolve_state(H2, O.evolve_state(H1, psi, [0, c["tau"]], cop), [0, c["tau"]], cop)
+    assert np.max(np.abs(out[0] - ref)) < TOL
