@@ -239,6 +239,61 @@ def pipelined_c2(params, protocol, n_steps, args, dev, n):
                     "a many-batch sweep's throughput, not the per-launch metric"}
 
 
+def end_to_end_c4(args, eng, host_params, t_host_derive):
+    """C4 end to end with the derivation on the device (hot-path row a1, ryd_derive): the
+    sweep's varying columns (species index, T, P_tweezer: 24 B per point) go to HBM once,
+    then each step derives the parameter block in HBM and propagates it.  Reported beside
+    the host derivation the kernel-only line starts from (physics.derive_batch +
+    pack_params, timed once) and checked against it at 1e-13 relative."""
+    from noisyquantumsimulator_amd import engine as E
+    from noisyquantumsimulator_amd import sweeps as SW
+    ws_, rk = (args.c4_shards, args.c4_rank) if args.c4_shards else (int(os.environ.get("WORLD_SIZE", 1)),
+                                                                   int(os.environ.get("RANK", 0)))
+    t0 = time.perf_counter()
+    inp = SW.c4_rank_inputs(rk, ws_)
+    t_cols = time.perf_counter() - t0
+    sw = E.DeviceSweep(eng, inp)
+    n = sw.n
+    ups = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        sw.upload()
+        ups.append(time.perf_counter() - t0)
+    for _ in range(max(args.warmup, 2)):
+        sw.launch()
+    sw.synchronize()
+    d_ms = float(np.mean([sw.derive(timed=True) for _ in range(5)]))
+    p_ms = float(np.mean([sw.propagate(timed=True) for _ in range(3)]))
+    sw.mark(0)
+    for _ in range(args.steps):
+        sw.launch()
+    sw.mark(1)
+    step_ms = sw.mark_elapsed() / args.steps
+    # with the inputs' H2D inside each step (host columns -> HBM -> derive -> engine)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sw.upload()
+        sw.launch()
+    sw.synchronize()
+    wh_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    pd, warn = sw.fetch_params()
+    rel = np.abs(pd - host_params) / np.maximum(np.abs(host_params), 1e-300)
+    rel[(pd == host_params)] = 0.0
+    res = sw.fetch()
+    assert np.all((res.status & E.N.STATUS_FAIL_MASK) == 0), "engine reported per-point failures"
+    sw.free()
+    return {"points": n, "derive_ms": d_ms, "engine_ms": p_ms, "derive_plus_engine_ms": step_ms,
+            "points_per_s": n / (step_ms * 1e-3),
+            "with_input_h2d_ms": wh_ms, "input_h2d_ms": float(np.median(ups)) * 1e3,
+            "input_bytes": int(inp.cols.nbytes), "host_columns_ms": t_cols * 1e3,
+            "host_derive_ms": t_host_derive * 1e3,
+            "device_vs_host_params_max_rel": float(rel.max()),
+            "note": ("derive_plus_engine_ms: ryd_derive_device + ryd_run_batch_device back to back on one "
+                     "stream, HIP events over K steps, inputs resident; with_input_h2d_ms adds the H2D of "
+                     "the varying columns each step (wall clock); host_derive_ms: the vectorised host "
+                     "derivation (physics.derive_batch) this replaces, one call")}
+
+
 def end_to_end_c2():
     """simulate_CZ_gate_batch on the C2 grid: derivation (host) + engine (host-buffer
     boundary) + the reference-penalty epilogue (zheevr on host threads, the batch call's
@@ -839,8 +894,10 @@ def main():
     else:
         # with --c4-shards: one rank's shard of an N-way split on this one GPU (the 1-GPU
         # strong-scaling proxy, as --c5-shards)
+        t_host_derive = time.perf_counter()
         batch = (SW.c4_rank_shard(args.c4_rank, args.c4_shards) if args.c4_shards
                  else SW.c4_rank_shard(rank, ws))
+        t_host_derive = time.perf_counter() - t_host_derive
         protocol, n_steps, n_seg = "lp_square", None, 2
         workload = ("C4: 1M-point species {Rb87, Cs133} x T logspace(1-100 uK, 1000) x P_tweezer "
                     "logspace(1-100 mW, 500) LP-square grid, range-sharded over the ranks, "
@@ -928,9 +985,12 @@ def main():
                  "host_unpack_gbs": bytes_d2h / (tl["unpack_ms"] * 1e-3) / 1e9, "calls": "median of 5 warm calls",
                  "staging": "persistent device workspace + pinned staging per handle slot; "
                             "unpack into the caller's strided numpy arrays on host threads"}
+    out_e2e = pipelined = None
     if args.workload == "c2" and ws == 1:
         out_e2e = end_to_end_c2()
         pipelined = pipelined_c2(params, protocol, n_steps, args, dev, n)
+    if args.workload == "c4":
+        out_e2e = end_to_end_c4(args, eng, params, t_host_derive)
     strong = args.workload == "c4"
     proxy = strong and args.c4_shards > 0
     global_points = n if proxy else (SW.C4_POINTS if strong else n * ws)
@@ -958,8 +1018,8 @@ def main():
                      "flops_per_launch": flops,
                      "exec_over_useful": res.matvec_exec / max(res.matvec_useful, 1)},
         "host_path": host_path,
-        "end_to_end": out_e2e if args.workload == "c2" and ws == 1 else None,
-        "pipelined": pipelined if args.workload == "c2" and ws == 1 else None,
+        "end_to_end": out_e2e,
+        "pipelined": pipelined,
         "roofline_hbm": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_launch": bytes_per_point * n},

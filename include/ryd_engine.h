@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RYD_ABI_VERSION 4
+#define RYD_ABI_VERSION 5
 
 /* ---- return codes ---- */
 #define RYD_OK              0
@@ -380,6 +380,146 @@ int ryd_lapack_pool(void* ref_zheevr, const char* path, const char* zheevr_symbo
 int ryd_evolve_generic(ryd_handle* h, int dim, int n_seg, int n_ops, int64_t n, int ket,
                        const double* H, const double* dt, const double* ops,
                        const double* state0, double* state_out, uint32_t* status);
+
+/* ---- hot-path row a1 on the device: parameter derivation (ryd_derive) ----
+ * The reference derives every point's physics on the host, one simulate_CZ_gate call at
+ * a time: steps 0-8 of RG/simulation.py:2761-3355 (Rabi frequencies RG/laser_physics.py:
+ * 111-427, blockade V = C6/R^6, the LP (Delta/Omega, Omega tau) lookup RG/protocols.py:
+ * 562-651 and xi :747-819, trap-dependent noise RG/trap_physics.py:1614-1848, Zeeman /
+ * Stark shifts :1851-2142, the noise rates :3230-3334 with RG/noise_models.py:483-963).
+ * ryd_derive evaluates the same formulas elementwise on the GPU, from per-point input
+ * fields straight into the engine's parameter block ([RYD_NPARAM][ld_params], the layout
+ * ryd_run_batch reads), so a 1M-point sweep (C4: species x T x P_tweezer) never builds
+ * its parameters on the host.  Each input field is either one value for every point
+ * (desc->value[f], desc->col[f] < 0) or row desc->col[f] of the caller's input block
+ * ([n_cols][ld_in] float64).  NaN means "not given" where the reference has a None
+ * default (linewidths, tweezer wavelength, background loss, LP delta/Omega and
+ * Omega tau, the signed smooth-JP delta/Omega); smooth-JP A / omega_mod_ratio / phi_offset
+ * of 0 take the defaults (the reference's `x or default`).  Species constants are the
+ * caller's table (noisyquantumsimulator_amd.species, RG/atom_database.py:104).
+ * Outputs: params (every column the protocol reads; the others 0), warn[i] = the
+ * RYD_STATUS_WEAK_BLOCKADE / DARK_STATE_SIGN / OMEGA_RANGE warning bits, and optionally
+ * the derived diagnostic columns diag [RYD_DV_NDIAG][ld_diag] (NULL = off). */
+#define RYD_DV_SPECIES      0   /* index into desc->species                              */
+#define RYD_DV_N_RYD        1
+#define RYD_DV_P1           2   /* laser 1 power W, waist m                              */
+#define RYD_DV_P2           3
+#define RYD_DV_W1           4
+#define RYD_DV_W2           5
+#define RYD_DV_DELTA_E      6   /* intermediate detuning rad/s                           */
+#define RYD_DV_LW1          7   /* laser linewidths Hz (NaN: None)                       */
+#define RYD_DV_LW2          8
+#define RYD_DV_TW_POWER     9
+#define RYD_DV_TW_WAIST     10
+#define RYD_DV_TW_WL_NM     11  /* NaN: the species' default trap wavelength             */
+#define RYD_DV_TEMPERATURE  12
+#define RYD_DV_B_FIELD      13
+#define RYD_DV_NA           14
+#define RYD_DV_SPACING      15
+#define RYD_DV_BG_LOSS      16  /* NaN: 1e3 /s                                           */
+#define RYD_DV_DOM          17  /* LP / smooth JP delta/Omega (NaN: lookup / default)    */
+#define RYD_DV_OMEGA_TAU    18  /* NaN: lookup / protocol default                        */
+#define RYD_DV_SJP_A        19  /* smooth JP A, omega_mod/Omega, phi_offset (0: default) */
+#define RYD_DV_SJP_OMR      20
+#define RYD_DV_SJP_PHI_OFF  21
+#define RYD_DV_SJP_SDOM     22  /* signed smooth-JP delta/Omega override (NaN: derived)  */
+#define RYD_DV_BB_SWT0      23  /* bang-bang switching times [7] and phases [8]          */
+#define RYD_DV_BB_PHI0      30
+#define RYD_DV_NFIELD       38
+/* species table row: mass, alpha_ground, trap_wavelength, n_ref, C6_ref, tau_0K_ref,
+ * tau_ref, alpha_rydberg_ref, dipole_er_ref, qd_S, dipole_1e, gamma_e, f_ground_to_e,
+ * E_ionization, omega_D1, K_quad_zeeman, K_quad_noise, stark_hz_per_mK, g_F_lower,
+ * F_lower, exp_C6, exp_tau0, exp_tau_bbr, exp_alpha */
+#define RYD_DV_NSPC         24
+#define RYD_DV_MAX_SPECIES  4
+/* flags */
+#define RYD_DV_NOISE        1u   /* include_noise                                          */
+#define RYD_DV_TRAP_ON      2u   /* trap_laser_on (Stark shift)                            */
+#define RYD_DV_DOPPLER      4u   /* NoiseSourceConfig.include_doppler_dephasing            */
+#define RYD_DV_INTENSITY    8u   /* include_intensity_noise                                */
+#define RYD_DV_COUNTERPROP  16u  /* TwoPhotonExcitationConfig.counter_propagating          */
+#define RYD_DV_MOTIONAL     32u  /* include_motional_dephasing                             */
+/* leakage spectral factor (RG/noise_models.py:732-853): the pulse shape's name */
+#define RYD_DV_LEAK_SQUARE   0
+#define RYD_DV_LEAK_GAUSSIAN 1
+#define RYD_DV_LEAK_COSINE   2
+#define RYD_DV_LEAK_BLACKMAN 3
+#define RYD_DV_LEAK_OTHER    4   /* smooth_sinusoidal, bangbang: sinc^2 with +1e-10       */
+/* diagnostic columns (the DerivedBatch fields of the same name) */
+#define RYD_DV_D_OMEGA1        0
+#define RYD_DV_D_OMEGA         1
+#define RYD_DV_D_V             2
+#define RYD_DV_D_R             3
+#define RYD_DV_D_U0            4
+#define RYD_DV_D_OMEGA_R       5
+#define RYD_DV_D_SIGMA_R       6
+#define RYD_DV_D_DVV           7
+#define RYD_DV_D_G_THERMAL     8
+#define RYD_DV_D_G_SCATTER     9
+#define RYD_DV_D_ALPHA_G       10
+#define RYD_DV_D_ALPHA_R       11
+#define RYD_DV_D_ALPHA_RATIO   12
+#define RYD_DV_D_G_ANTITRAP    13
+#define RYD_DV_D_DIFF_SHIFT    14
+#define RYD_DV_D_ENHANCEMENT   15
+#define RYD_DV_D_K_EFF         16
+#define RYD_DV_D_V_THERMAL     17
+#define RYD_DV_D_G_DOPPLER     18
+#define RYD_DV_D_G_INTENSITY   19
+#define RYD_DV_D_GAMMA_R_TRAP  20
+#define RYD_DV_D_WAVELENGTH_NM 21
+#define RYD_DV_D_TAU_SINGLE    22
+#define RYD_DV_D_TAU_TOTAL     23
+#define RYD_DV_D_DELTA_GATE    24
+#define RYD_DV_D_DOM           25
+#define RYD_DV_D_OMEGA_TAU     26
+#define RYD_DV_D_DELTA_ZEEMAN  27
+#define RYD_DV_D_DELTA_STARK   28
+#define RYD_DV_D_V_OVER_OMEGA  29
+#define RYD_DV_D_XI_RE         30
+#define RYD_DV_D_XI_IM         31
+#define RYD_DV_D_DELTA_SEG     32
+#define RYD_DV_D_GAMMA_R       33   /* the noise rates (0 without include_noise)          */
+#define RYD_DV_D_GAMMA_PHI_LASER   34
+#define RYD_DV_D_GAMMA_PHI_THERMAL 35
+#define RYD_DV_D_GAMMA_PHI_ZEEMAN  36
+#define RYD_DV_D_GAMMA_LOSS_ANTITRAP 37
+#define RYD_DV_D_GAMMA_LOSS_BG     38
+#define RYD_DV_D_GAMMA_LEAKAGE     39
+#define RYD_DV_D_GAMMA_SCATTER     40
+#define RYD_DV_D_MJ_RATE           41
+#define RYD_DV_D_AREA_CORR         42
+#define RYD_DV_NDIAG           43
+
+typedef struct ryd_derive_desc {
+  int32_t abi_version;       /* = RYD_ABI_VERSION */
+  int32_t protocol;          /* RYD_PROTO_* */
+  int32_t shape;             /* RYD_SHAPE_* (LP_SHAPED: area correction) */
+  int32_t leak_shape;        /* RYD_DV_LEAK_* */
+  int32_t dim;               /* 3 | 4 (dim 4: the mJ-mixing rate columns) */
+  uint32_t flags;            /* RYD_DV_* flags */
+  int32_t n_species;         /* rows of species[] in use */
+  int32_t bb_nseg;           /* bang-bang segments (= phases), 0 otherwise */
+  double qubit[4];           /* F0, mF0, F1, mF1 */
+  double intensity_noise_frac;
+  double polarization_purity;  /* min of the two lasers' (dim 4) */
+  double species[RYD_DV_MAX_SPECIES][RYD_DV_NSPC];
+  double value[RYD_DV_NFIELD];
+  int32_t col[RYD_DV_NFIELD];
+} ryd_derive_desc;
+
+/* Device form: d_in [n_cols][ld_in] on slot `slot` (may be NULL if every col < 0);
+ * d_params [RYD_NPARAM][ld_params]; d_warn [n]; d_diag nullable.  Enqueues on `stream`
+ * (NULL: the slot's stream); elapsed_ms as ryd_run_batch_device. */
+int ryd_derive_device(ryd_handle* h, int slot, const ryd_derive_desc* desc,
+                      const double* d_in, int64_t ld_in, int64_t n,
+                      double* d_params, int64_t ld_params, uint32_t* d_warn,
+                      double* d_diag, int64_t ld_diag, void* stream, float* elapsed_ms);
+/* Host form (blocking, the handle's first device): in [n_cols][ld_in] host (NULL if every
+ * col < 0), params [RYD_NPARAM][ld_params], warn [n], diag nullable. */
+int ryd_derive(ryd_handle* h, const ryd_derive_desc* desc, const double* in, int64_t n_cols,
+               int64_t ld_in, int64_t n, double* params, int64_t ld_params, uint32_t* warn,
+               double* diag, int64_t ld_diag);
 
 /* Timeline of the handle's last host-buffer call (ryd_run_batch / _coherences /
  * _trajectories).  Those calls keep a device workspace and a pinned host staging buffer

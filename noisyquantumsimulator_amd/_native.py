@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RYD_ENGINE_LIB") or os.path.join(_HERE, "libryd_engine.so")
 
 # keep in sync with include/ryd_engine.h
-RYD_ABI_VERSION = 4
+RYD_ABI_VERSION = 5
 RYD_OK = 0
 PROTO = {"lp_square": 0, "lp_shaped": 1, "bangbang": 2, "smooth_jp": 3}
 EVOL = {"lindblad": 0, "ket": 1}
@@ -60,7 +60,32 @@ EXPORTED = ("ryd_abi_version", "ryd_last_error", "ryd_param_count", "ryd_summary
             "ryd_run_batch_device", "ryd_run_coherences", "ryd_run_coherences_device",
             "ryd_run_trajectories", "ryd_run_trajectories_device",
             "ryd_mixed_phase", "ryd_lapack_pool", "ryd_last_timeline", "ryd_mark", "ryd_mark_elapsed",
-            "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize", "ryd_evolve_generic")
+            "ryd_malloc", "ryd_free", "ryd_memcpy_h2d", "ryd_memcpy_d2h", "ryd_synchronize", "ryd_evolve_generic",
+            "ryd_derive", "ryd_derive_device")
+
+# device derivation (ryd_derive): input fields, species-table columns, flags, diagnostic columns
+DV = dict(SPECIES=0, N_RYD=1, P1=2, P2=3, W1=4, W2=5, DELTA_E=6, LW1=7, LW2=8, TW_POWER=9, TW_WAIST=10,
+          TW_WL_NM=11, TEMPERATURE=12, B_FIELD=13, NA=14, SPACING=15, BG_LOSS=16, DOM=17, OMEGA_TAU=18,
+          SJP_A=19, SJP_OMR=20, SJP_PHI_OFF=21, SJP_SDOM=22, BB_SWT0=23, BB_PHI0=30)
+DV_NFIELD = 38
+DV_NSPC = 24
+DV_MAX_SPECIES = 4
+DV_SPC = ("mass", "alpha_ground", "trap_wavelength", "n_ref", "C6_ref", "tau_0K_ref", "tau_ref",
+          "alpha_rydberg_ref", "dipole_er_ref", "qd_S", "dipole_1e", "gamma_e", "f_ground_to_e", "E_ionization",
+          "omega_D1", "K_quad_zeeman", "K_quad_noise", "stark_hz_per_mK", "g_F_lower", "F_lower", "exp_C6",
+          "exp_tau0", "exp_tau_bbr", "exp_alpha")
+DV_FLAG = dict(NOISE=1, TRAP_ON=2, DOPPLER=4, INTENSITY=8, COUNTERPROP=16, MOTIONAL=32)
+DV_LEAK = dict(square=0, gaussian=1, cosine=2, blackman=3)          # anything else: 4 (sinc^2 + 1e-10)
+DV_LEAK_OTHER = 4
+# diagnostic columns -> the DerivedBatch column of the same quantity
+DV_DIAG = ("Omega1", "Omega", "V", "R", "U0", "omega_r", "sigma_r", "dVV", "g_thermal", "g_scatter", "alpha_g",
+           "alpha_r", "alpha_ratio", "g_antitrap_raw", "diff_shift", "enhancement", "k_eff", "v_thermal",
+           "g_doppler", "g_intensity", "gamma_r_trap", "wavelength_nm", "tau_single", "tau_total", "Delta_gate",
+           "delta_over_omega", "omega_tau", "delta_zeeman", "delta_stark", "V_over_Omega", "xi_re", "xi_im",
+           "Delta_seg", "gamma_r", "gamma_phi_laser", "gamma_phi_thermal", "gamma_phi_zeeman",
+           "gamma_loss_antitrap", "gamma_loss_background", "gamma_leakage", "gamma_scatter_intermediate",
+           "mJ_leakage_rate", "area_correction")
+DV_NDIAG = len(DV_DIAG)
 
 
 class BatchDesc(ctypes.Structure):
@@ -77,6 +102,15 @@ class TrajDesc(ctypes.Structure):
                 ("shape", ctypes.c_int32), ("n_steps", ctypes.c_int32),
                 ("n_traj", ctypes.c_int32), ("ladder_levels", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("psi0", ctypes.c_double * 54)]
+
+
+class DeriveDesc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("protocol", ctypes.c_int32), ("shape", ctypes.c_int32),
+                ("leak_shape", ctypes.c_int32), ("dim", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("n_species", ctypes.c_int32), ("bb_nseg", ctypes.c_int32), ("qubit", ctypes.c_double * 4),
+                ("intensity_noise_frac", ctypes.c_double), ("polarization_purity", ctypes.c_double),
+                ("species", (ctypes.c_double * DV_NSPC) * DV_MAX_SPECIES),
+                ("value", ctypes.c_double * DV_NFIELD), ("col", ctypes.c_int32 * DV_NFIELD)]
 
 
 class Stats(ctypes.Structure):
@@ -141,6 +175,10 @@ def load() -> ctypes.CDLL:
         lib.ryd_synchronize.argtypes = [vp]
         lib.ryd_evolve_generic.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, dp, dp,
                                            dp, dp, dp, ctypes.POINTER(ctypes.c_uint32)]
+        lib.ryd_derive.argtypes = [vp, ctypes.POINTER(DeriveDesc), dp, i64, i64, i64, dp, i64,
+                                   ctypes.POINTER(ctypes.c_uint32), dp, i64]
+        lib.ryd_derive_device.argtypes = [vp, ctypes.c_int, ctypes.POINTER(DeriveDesc), vp, i64, i64, vp, i64, vp,
+                                          vp, i64, vp, ctypes.POINTER(ctypes.c_float)]
         if lib.ryd_abi_version() != RYD_ABI_VERSION:
             raise EngineError("libryd_engine.so ABI version mismatch; rebuild it")
         if lib.ryd_param_count() != NPARAM or lib.ryd_summary_width() != NSUMMARY:

@@ -3040,6 +3040,9 @@ int run_partitioned(ryd_handle* h, const double* params, int64_t n, int64_t ld_p
 #include "ryd_traj.inc"
 #include "ryd_generic.inc"
 
+// hot-path row a1 on the device: parameter derivation (ryd_derive)
+#include "ryd_derive.inc"
+
 // host epilogue: the reference's mixed-state controlled phase (ryd_mixed_phase)
 #include "ryd_epilogue.inc"
 
@@ -3127,6 +3130,9 @@ int ryd_free(ryd_handle* h, int slot, void* p) {
 int ryd_memcpy_h2d(ryd_handle* h, int slot, void* dst, const void* src, size_t bytes) {
   if (!h || slot < 0 || slot >= (int)h->dev.size()) return fail(RYD_ERR_INVALID, "bad args");
   HIPCHK(hipSetDevice(h->dev[slot]));
+  // the slot's earlier work first: a copy to or from pageable memory is not reliably
+  // ordered behind the kernels already on the stream
+  HIPCHK(hipStreamSynchronize(h->stream[slot]));
   HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, h->stream[slot]));
   HIPCHK(hipStreamSynchronize(h->stream[slot]));
   return RYD_OK;
@@ -3135,6 +3141,9 @@ int ryd_memcpy_h2d(ryd_handle* h, int slot, void* dst, const void* src, size_t b
 int ryd_memcpy_d2h(ryd_handle* h, int slot, void* dst, const void* src, size_t bytes) {
   if (!h || slot < 0 || slot >= (int)h->dev.size()) return fail(RYD_ERR_INVALID, "bad args");
   HIPCHK(hipSetDevice(h->dev[slot]));
+  // the slot's earlier work first: a copy to or from pageable memory is not reliably
+  // ordered behind the kernels already on the stream
+  HIPCHK(hipStreamSynchronize(h->stream[slot]));
   HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, h->stream[slot]));
   HIPCHK(hipStreamSynchronize(h->stream[slot]));
   return RYD_OK;
@@ -3355,6 +3364,69 @@ int ryd_run_coherences_device(ryd_handle* h, int slot, const ryd_batch_desc* des
   rc = launch_coherences(desc, d_params, n, ld_params, d_coh, ld_coh, d_status, s);
   if (rc) return rc;
   return elapsed_ms ? timer.stop(s, elapsed_ms) : RYD_OK;
+}
+
+int ryd_derive_device(ryd_handle* h, int slot, const ryd_derive_desc* desc, const double* d_in, int64_t ld_in,
+                      int64_t n, double* d_params, int64_t ld_params, uint32_t* d_warn, double* d_diag,
+                      int64_t ld_diag, void* stream, float* elapsed_ms) {
+  if (!h || slot < 0 || slot >= (int)h->dev.size()) return fail(RYD_ERR_INVALID, "bad handle/slot");
+  HIPCHK(hipSetDevice(h->dev[slot]));
+  hipStream_t s = stream ? (hipStream_t)stream : h->stream[slot];
+  LaunchTimer timer;
+  int rc;
+  if (elapsed_ms) {
+    rc = timer.start(s);
+    if (rc) return rc;
+  }
+  rc = launch_derive(desc, d_in, ld_in, n, d_params, ld_params, d_warn, d_diag, ld_diag, s);
+  if (rc) return rc;
+  return elapsed_ms ? timer.stop(s, elapsed_ms) : RYD_OK;
+}
+
+int ryd_derive(ryd_handle* h, const ryd_derive_desc* desc, const double* in, int64_t n_cols, int64_t ld_in,
+               int64_t n, double* params, int64_t ld_params, uint32_t* warn, double* diag, int64_t ld_diag) {
+  if (!h || h->dev.empty() || !desc) return fail(RYD_ERR_INVALID, "derive: NULL handle/desc");
+  if (n < 0 || n_cols < 0 || ld_params < n || (diag && ld_diag < n) || (n_cols > 0 && (!in || ld_in < n)))
+    return fail(RYD_ERR_INVALID, "derive: bad sizes");
+  for (int f = 0; f < RYD_DV_NFIELD; ++f)
+    if (desc->col[f] >= n_cols) return fail(RYD_ERR_INVALID, "derive: a field's column is beyond n_cols");
+  if (n == 0) return RYD_OK;
+  if (!params || !warn) return fail(RYD_ERR_INVALID, "derive: NULL output");
+  const int dev = h->dev[0];
+  hipStream_t s = h->stream[0];
+  HIPCHK(hipSetDevice(dev));
+  hipMemPool_t pool = jp_pool(dev);
+  if (!pool) return fail(RYD_ERR_ALLOC, "derive: pool creation failed");
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t bIn = sizeof(double) * (size_t)n_cols * n, bP = sizeof(double) * RYD_NPARAM * (size_t)n,
+               bW = sizeof(uint32_t) * (size_t)n, bD = diag ? sizeof(double) * RYD_DV_NDIAG * (size_t)n : 0;
+  const size_t oP = al(bIn), oW = oP + al(bP), oD = oW + al(bW), tot = oD + al(bD) + 256;
+  // pageable host buffers: every copy is a blocking hipMemcpy issued after the stream work it
+  // depends on has completed (an async copy to or from pageable memory was observed to run
+  // ahead of the kernel on the same stream)
+  char* buf = nullptr;
+  HIPCHK(hipMallocFromPoolAsync((void**)&buf, tot, pool, s));
+  hipError_t e = hipStreamSynchronize(s);
+  for (int64_t c = 0; c < n_cols && e == hipSuccess; ++c)
+    e = hipMemcpy(buf + sizeof(double) * (size_t)c * n, in + c * ld_in, sizeof(double) * n, hipMemcpyHostToDevice);
+  int rc = RYD_OK;
+  if (e == hipSuccess)
+    rc = launch_derive(desc, (const double*)buf, n, n, (double*)(buf + oP), n, (uint32_t*)(buf + oW),
+                       diag ? (double*)(buf + oD) : nullptr, n, s);
+  if (e == hipSuccess && rc == RYD_OK) e = hipStreamSynchronize(s);
+  for (int f = 0; f < RYD_NPARAM && e == hipSuccess && rc == RYD_OK; ++f)
+    e = hipMemcpy(params + f * ld_params, buf + oP + sizeof(double) * (size_t)f * n, sizeof(double) * n,
+                  hipMemcpyDeviceToHost);
+  if (e == hipSuccess && rc == RYD_OK) e = hipMemcpy(warn, buf + oW, bW, hipMemcpyDeviceToHost);
+  for (int k = 0; diag && k < RYD_DV_NDIAG && e == hipSuccess && rc == RYD_OK; ++k)
+    e = hipMemcpy(diag + k * ld_diag, buf + oD + sizeof(double) * (size_t)k * n, sizeof(double) * n,
+                  hipMemcpyDeviceToHost);
+  const hipError_t ef = hipFreeAsync(buf, s);
+  const hipError_t es = hipStreamSynchronize(s);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(RYD_ERR_HIP, std::string("derive: ") + hipGetErrorString(e));
+  if (ef != hipSuccess || es != hipSuccess) return fail(RYD_ERR_HIP, "derive: free/sync failed");
+  return RYD_OK;
 }
 
 }  // extern "C"

@@ -304,6 +304,22 @@ class Engine:
         return coh, status
 
 
+    def derive(self, inp, diag: bool = False) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray]]:
+        """Hot-path row a1 on the GPU (ryd_derive): ``physics.derive_inputs(...)`` ->
+        (params (NPARAM, n) as pack_params builds them, warning bits (n,) uint32, and with
+        ``diag`` the (DV_NDIAG, n) derived columns named by _native.DV_DIAG)."""
+        n = inp.n
+        cols = np.ascontiguousarray(inp.cols, dtype=np.float64)
+        params = np.empty((N.NPARAM, n), dtype=np.float64)
+        warn = np.zeros(n, dtype=np.uint32)
+        dg = np.empty((N.DV_NDIAG, n), dtype=np.float64) if diag else None
+        dptr = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+        N.check(self.lib.ryd_derive(self.handle, ctypes.byref(inp.desc), dptr(cols) if cols.shape[0] else None,
+                                    cols.shape[0], n, n, dptr(params), n,
+                                    warn.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                    dptr(dg) if diag else None, n))
+        return params, warn, dg
+
     def evolve_generic(self, H: np.ndarray, dt: np.ndarray, state0: np.ndarray,
                        ops: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
         """The generic evolve_state seam (ryd_evolve_generic; RG/simulation.py:647-690) for
@@ -396,6 +412,105 @@ class DeviceBatch:
         N.check(lib.ryd_memcpy_d2h(h, s, summ.ctypes.data, self.d_summary, summ.nbytes))
         N.check(lib.ryd_memcpy_d2h(h, s, status.ctypes.data, self.d_status, status.nbytes))
         return EngineResult(self.evolution, self.n, state, summ, status, 0.0, 0.0, 0.0,
+                            summ[N.S["NMV_USEFUL"]].sum(), summ[N.S["NMV_EXEC"]].sum(), self.dim)
+
+    def free(self):
+        for p in self._bufs:
+            self.eng.lib.ryd_free(self.eng.handle, self.slot, p)
+        self._bufs = []
+
+
+class DeviceSweep:
+    """A sweep whose parameters never exist on the host: its varying input fields are
+    resident on one device slot (``upload``), ``ryd_derive_device`` writes the parameter
+    block in HBM and the propagation kernel reads it there (C4: 1M species x T x
+    P_tweezer points -> derive + engine on the device).  ``launch`` enqueues derive then
+    engine on the slot's stream."""
+
+    def __init__(self, engine: Engine, inp, evolution: str = "lindblad", slot: int = 0,
+                 n_steps: Optional[int] = None, method: str = "chebyshev"):
+        self.eng, self.slot, self.inp = engine, slot, inp
+        lib = engine.lib
+        self.n = n = inp.n
+        self.dim = inp.dim
+        self.width = N.STATE_WIDTH_DIM[inp.dim][evolution]
+        self.evolution = evolution
+        if n_steps is None:
+            n_steps = {"smooth_jp": 300, "lp_shaped": 500}.get(inp.protocol, 0)
+            if inp.protocol == "bangbang":
+                n_steps = int(inp.desc.bb_nseg)
+        # every shared rate is equal on both atoms (the derivation writes atom B = atom A)
+        self.desc = make_desc(inp.protocol, evolution, n_steps, inp.shape, True, method, dim=inp.dim)
+        self._bufs = []
+
+        def alloc(nbytes):
+            p = ctypes.c_void_p()
+            N.check(lib.ryd_malloc(engine.handle, slot, max(nbytes, 16), ctypes.byref(p)))
+            self._bufs.append(p)
+            return p
+        self.k = inp.cols.shape[0]
+        self.d_in = alloc(8 * self.k * n)
+        self.d_params = alloc(8 * N.NPARAM * n)
+        self.d_warn = alloc(4 * n)
+        self.d_state = alloc(8 * self.width * 4 * n)
+        self.d_summary = alloc(8 * N.NSUMMARY * n)
+        self.d_status = alloc(4 * n)
+        self.upload()
+
+    def upload(self):
+        """H2D of the varying input fields (the only per-point host data)."""
+        cols = np.ascontiguousarray(self.inp.cols, dtype=np.float64)
+        if self.k:
+            N.check(self.eng.lib.ryd_memcpy_h2d(self.eng.handle, self.slot, self.d_in, cols.ctypes.data, cols.nbytes))
+
+    def derive(self, timed: bool = False) -> float:
+        ms = ctypes.c_float(0.0)
+        N.check(self.eng.lib.ryd_derive_device(
+            self.eng.handle, self.slot, ctypes.byref(self.inp.desc), self.d_in if self.k else None, self.n,
+            self.n, self.d_params, self.n, self.d_warn, None, self.n, None, ctypes.byref(ms) if timed else None))
+        return float(ms.value)
+
+    def propagate(self, timed: bool = False) -> float:
+        ms = ctypes.c_float(0.0)
+        N.check(self.eng.lib.ryd_run_batch_device(
+            self.eng.handle, self.slot, ctypes.byref(self.desc), self.d_params, self.n, self.n,
+            self.d_state, 4 * self.n, self.d_summary, self.n, self.d_status, None,
+            ctypes.byref(ms) if timed else None))
+        return float(ms.value)
+
+    def launch(self):
+        self.derive()
+        self.propagate()
+
+    def mark(self, which: int):
+        N.check(self.eng.lib.ryd_mark(self.eng.handle, self.slot, which))
+
+    def mark_elapsed(self) -> float:
+        ms = ctypes.c_float(0.0)
+        N.check(self.eng.lib.ryd_mark_elapsed(self.eng.handle, self.slot, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def synchronize(self):
+        N.check(self.eng.lib.ryd_synchronize(self.eng.handle))
+
+    def fetch_params(self) -> Tuple[np.ndarray, np.ndarray]:
+        lib, h, s = self.eng.lib, self.eng.handle, self.slot
+        p = np.zeros((N.NPARAM, self.n))
+        w = np.zeros(self.n, dtype=np.uint32)
+        N.check(lib.ryd_memcpy_d2h(h, s, p.ctypes.data, self.d_params, p.nbytes))
+        N.check(lib.ryd_memcpy_d2h(h, s, w.ctypes.data, self.d_warn, w.nbytes))
+        return p, w
+
+    def fetch(self) -> EngineResult:
+        lib, h, s = self.eng.lib, self.eng.handle, self.slot
+        state = np.zeros((self.width, 4 * self.n))
+        summ = np.zeros((N.NSUMMARY, self.n))
+        status = np.zeros(self.n, dtype=np.uint32)
+        N.check(lib.ryd_memcpy_d2h(h, s, state.ctypes.data, self.d_state, state.nbytes))
+        N.check(lib.ryd_memcpy_d2h(h, s, summ.ctypes.data, self.d_summary, summ.nbytes))
+        N.check(lib.ryd_memcpy_d2h(h, s, status.ctypes.data, self.d_status, status.nbytes))
+        _, warn = self.fetch_params()
+        return EngineResult(self.evolution, self.n, state, summ, status | warn, 0.0, 0.0, 0.0,
                             summ[N.S["NMV_USEFUL"]].sum(), summ[N.S["NMV_EXEC"]].sum(), self.dim)
 
     def free(self):

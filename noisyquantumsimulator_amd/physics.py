@@ -488,6 +488,161 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
                         noise_config=noise, status_bits=bits)
 
 
+@dataclass
+class DeriveInputs:
+    """Inputs of the device derivation (ryd_derive): the descriptor (shared values,
+    flags, species table) and the per-point input block [k][n] of the fields that vary."""
+    desc: Any                       # _native.DeriveDesc
+    cols: np.ndarray                # (k, n) float64
+    n: int
+    protocol: str                   # lp_square | lp_shaped | smooth_jp | bangbang (engine key)
+    shape: str
+    dim: int
+    include_noise: bool
+
+
+_NONE = float("nan")
+
+
+def derive_inputs(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
+                  n_rydberg=70, qubit_0=(1, 0), qubit_1=(2, 0), hilbert_space_dim: int = 3,
+                  tweezer_power=30e-3, tweezer_waist=1.0e-6, tweezer_wavelength_nm=None,
+                  temperature=2e-6, B_field=1e-4, NA=0.5, spacing_factor=2.8,
+                  include_noise: bool = True, background_loss_rate_hz=None,
+                  trap_laser_on: bool = True, overrides: Optional[Dict[str, Any]] = None) -> DeriveInputs:
+    """The arguments of ``derive_batch`` as ryd_derive inputs: every argument that is an
+    array becomes a row of the input block, every scalar a descriptor value (so a C4 sweep
+    ships only its species, T and P_tweezer columns).  Same validation and defaults as
+    ``derive_batch``; the device evaluates the same formulas (csrc/ryd_derive.inc)."""
+    from . import _native as N
+    from .configurations import (JPSimulationInputs, LPSimulationInputs,
+                                 SmoothJPSimulationInputs)
+    ov = dict(overrides or {})
+    si = simulation_inputs
+    if isinstance(si, LPSimulationInputs):
+        pulse_shape = si.pulse_shape
+        shape = pulse_shape.lower()
+        if shape == "drag":
+            raise TypeError("pulse_envelope_drag() missing 1 required positional argument: 'Delta_leak'")
+        if shape not in N.SHAPE:
+            raise ValueError(f"Unknown pulse shape: {pulse_shape}. "
+                             f"Available shapes: ['square', 'gaussian', 'cosine', 'blackman', 'drag']")
+        proto = "lp_square" if shape == "square" else "lp_shaped"
+    elif isinstance(si, SmoothJPSimulationInputs):
+        proto, pulse_shape, shape = "smooth_jp", "smooth_sinusoidal", "square"
+    elif isinstance(si, JPSimulationInputs):
+        proto, pulse_shape, shape = "bangbang", "bangbang", "square"
+    else:
+        raise TypeError("simulation_inputs must be LPSimulationInputs, JPSimulationInputs, "
+                        f"or SmoothJPSimulationInputs, got {type(si).__name__}")
+    if hilbert_space_dim not in (3, 4):
+        raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
+    exc, noise = si.excitation, si.noise
+    L1, L2 = exc.laser_1, exc.laser_2
+    De = ov.get("Delta_e", exc.Delta_e)
+    if De is None or np.any(np.isnan(np.asarray(De, dtype=float))):
+        raise TypeError("TwoPhotonExcitationConfig.Delta_e must be a number")
+    names = list(S.SPECIES)
+    sp_arr = np.asarray(species)
+    if np.issubdtype(sp_arr.dtype, np.integer):        # indices into the species table (sweeps)
+        if sp_arr.size and (sp_arr.min() < 0 or sp_arr.max() >= len(names)):
+            raise ValueError(f"species index out of range: the table is {names}")
+        sp_idx = sp_arr.astype(float) if sp_arr.ndim else float(sp_arr)
+    elif sp_arr.ndim:
+        u, inv = np.unique(sp_arr, return_inverse=True)
+        sp_idx = np.array([names.index(S.get(str(nm)).name) for nm in u], dtype=float)[inv.ravel()]
+    else:
+        sp_idx = float(names.index(S.get(str(species)).name))
+    fields = {
+        "SPECIES": sp_idx, "N_RYD": n_rydberg,
+        "P1": ov.get("laser_1_power", L1.power), "P2": ov.get("laser_2_power", L2.power),
+        "W1": ov.get("laser_1_waist", L1.waist), "W2": ov.get("laser_2_waist", L2.waist),
+        "DELTA_E": ov.get("Delta_e", exc.Delta_e),
+        "LW1": ov.get("laser_1_linewidth_hz", L1.linewidth_hz), "LW2": ov.get("laser_2_linewidth_hz", L2.linewidth_hz),
+        "TW_POWER": tweezer_power, "TW_WAIST": tweezer_waist, "TW_WL_NM": tweezer_wavelength_nm,
+        "TEMPERATURE": temperature, "B_FIELD": B_field, "NA": NA, "SPACING": spacing_factor,
+        "BG_LOSS": background_loss_rate_hz,
+    }
+    dv_ = ov.get("delta_over_omega", getattr(si, "delta_over_omega", None))
+    otv = ov.get("omega_tau", si.omega_tau)
+    fields["DOM"], fields["OMEGA_TAU"] = dv_, otv
+    nseg = 0
+    if proto == "smooth_jp":
+        for key, attr, f in (("A", "A", "SJP_A"), ("omega_mod_ratio", "omega_mod_ratio", "SJP_OMR"),
+                             ("phi_offset", "phi_offset", "SJP_PHI_OFF")):
+            v = ov.get(key, getattr(si, attr))
+            fields[f] = v if v is not None else 0.0
+        fields["SJP_SDOM"] = ov.get("smooth_delta_over_omega")
+    elif proto == "bangbang":
+        def _or_default(v, default):
+            if isinstance(v, np.ndarray):
+                return v if v.size else list(default)
+            return v or list(default)
+        st = np.asarray(_or_default(ov.get("switching_times", si.switching_times), P.JP_BANGBANG_SWITCHING_TIMES),
+                        dtype=float)
+        ph = np.asarray(_or_default(ov.get("phases", si.phases), P.JP_BANGBANG_PHASES), dtype=float)
+        if ph.shape[-1] != st.shape[-1] + 1:
+            raise AssertionError(f"Need len(phases) = len(switching_times) + 1, got "
+                                 f"{ph.shape[-1]} phases and {st.shape[-1]} switching times")
+        nseg = ph.shape[-1]
+        if nseg > 8:
+            raise ValueError("bang-bang schedules with more than 8 segments are not supported")
+        for k in range(nseg - 1):
+            fields[f"BB_SWT{k}"] = st[..., k]
+        for k in range(nseg):
+            fields[f"BB_PHI{k}"] = ph[..., k]
+    sizes = [np.shape(v)[0] for v in fields.values() if v is not None and np.ndim(v) > 0]
+    if n is None:
+        n = max(sizes) if sizes else 1
+    desc = N.DeriveDesc()
+    desc.abi_version = N.RYD_ABI_VERSION
+    desc.protocol = N.PROTO[proto]
+    desc.shape = N.SHAPE[shape]
+    desc.leak_shape = N.DV_LEAK.get(pulse_shape, N.DV_LEAK_OTHER)
+    desc.dim = hilbert_space_dim
+    fl = N.DV_FLAG
+    desc.flags = ((fl["NOISE"] if include_noise else 0) | (fl["TRAP_ON"] if trap_laser_on else 0)
+                  | (fl["DOPPLER"] if noise.include_doppler_dephasing else 0)
+                  | (fl["INTENSITY"] if noise.include_intensity_noise else 0)
+                  | (fl["COUNTERPROP"] if exc.counter_propagating else 0)
+                  | (fl["MOTIONAL"] if noise.include_motional_dephasing else 0))
+    desc.n_species = len(names)
+    desc.bb_nseg = nseg
+    desc.qubit[:] = [float(qubit_0[0]), float(qubit_0[1]), float(qubit_1[0]), float(qubit_1[1])]
+    desc.intensity_noise_frac = float(noise.intensity_noise_frac)
+    desc.polarization_purity = float(min(L1.polarization_purity, L2.polarization_purity))
+    for r, nm in enumerate(names):
+        spc = S.SPECIES[nm]
+        for c, k in enumerate(N.DV_SPC):
+            desc.species[r][c] = float(getattr(spc, k))
+    rows = []
+    for k in range(N.DV_NFIELD):
+        desc.col[k] = -1
+        desc.value[k] = 0.0
+    idx = {}
+    for k, v in N.DV.items():
+        idx[k] = v
+    for k in range(7):
+        idx[f"BB_SWT{k}"] = N.DV["BB_SWT0"] + k
+    for k in range(8):
+        idx[f"BB_PHI{k}"] = N.DV["BB_PHI0"] + k
+    for k, v in fields.items():
+        f = idx[k]
+        if v is None:
+            desc.value[f] = _NONE
+        elif np.ndim(v) > 0:
+            a = np.broadcast_to(np.asarray(v, dtype=float), (n,))
+            desc.col[f] = len(rows)
+            rows.append(a)
+        else:
+            desc.value[f] = float(v)
+    if proto == "smooth_jp" and np.ndim(fields["DOM"]) == 0 and fields["DOM"] is None:
+        desc.value[N.DV["DOM"]] = _NONE
+    cols = np.ascontiguousarray(np.stack(rows)) if rows else np.zeros((0, n))
+    return DeriveInputs(desc=desc, cols=cols, n=n, protocol=proto, shape=shape, dim=hilbert_space_dim,
+                        include_noise=include_noise)
+
+
 def area_correction_factor(pulse_shape: str, tau) -> np.ndarray:
     """Peak-Omega scale of a shaped LP pulse (RG/pulse_shaping.py:795-842): the
     square area tau over the trapezoid area of the envelope on linspace(0, tau, 1000).

@@ -142,6 +142,36 @@ def species_temperature_power_grid(n_T: int = 1000, n_P: int = 500, include_nois
                            include_noise=include_noise)
 
 
+def c4_columns(n_T: int = 1000, n_P: int = 500, point_slice: Optional[slice] = None):
+    """The C4 grid's varying columns (species-table index: 0 Rb87, 1 Cs133; T; P_tweezer),
+    species-major."""
+    T = np.logspace(-6, -4, n_T)
+    P = np.logspace(-3, -1, n_P)
+    S_, T_, P_ = np.meshgrid(np.arange(2), T, P, indexing="ij")
+    S_, T_, P_ = S_.ravel(), T_.ravel(), P_.ravel()
+    if point_slice is not None:
+        S_, T_, P_ = S_[point_slice], T_[point_slice], P_[point_slice]
+    return S_, T_, P_
+
+
+def species_temperature_power_inputs(n_T: int = 1000, n_P: int = 500, include_noise: bool = True,
+                                     point_slice: Optional[slice] = None) -> PH.DeriveInputs:
+    """C4 as device-derivation inputs (ryd_derive): the same points as
+    species_temperature_power_grid, but only the species / T / P_tweezer columns travel;
+    every other field is a descriptor value, and the parameters are derived in HBM."""
+    warnings.simplefilter("ignore")
+    sp, T_, P_ = c4_columns(n_T, n_P, point_slice)
+    return PH.derive_inputs(CF.LPSimulationInputs(excitation=medium_excitation()), n=T_.size,
+                            **_apparatus_kwargs(species=sp, temperature=T_, tweezer_power=P_),
+                            include_noise=include_noise)
+
+
+def c4_rank_inputs(rank: int, world_size: int, include_noise: bool = True) -> PH.DeriveInputs:
+    """Rank r's contiguous range of the 1M-point C4 grid as device-derivation inputs."""
+    return species_temperature_power_inputs(include_noise=include_noise,
+                                            point_slice=range_shard(C4_POINTS, rank, world_size))
+
+
 # C1 (SURVEY.md §8d): one dim-3 LP-square point, Omega = 2 pi 5 MHz, V/Omega = 100, the LP
 # defaults Delta/Omega = 0.377371 and Omega tau = 4.29268, xi from compute_phase_shift_xi,
 # one collapse operator sqrt(gamma) |1><r| (x) I with gamma = 1/140 us (Rb87 n = 70)

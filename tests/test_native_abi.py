@@ -42,6 +42,19 @@ def test_header_constants_match_binding():
     assert int(defs["RYD_T_NSUMMARY"]) == N.T_NSUMMARY
     assert int(defs["RYD_ABI_VERSION"]) == N.RYD_ABI_VERSION
     assert ctypes.sizeof(N.TrajDesc) == 464
+    for k, v in N.DV.items():
+        assert int(defs["RYD_DV_" + k]) == v
+    assert int(defs["RYD_DV_NFIELD"]) == N.DV_NFIELD and int(defs["RYD_DV_NSPC"]) == N.DV_NSPC
+    assert int(defs["RYD_DV_MAX_SPECIES"]) == N.DV_MAX_SPECIES and len(N.DV_SPC) == N.DV_NSPC
+    for k, v in N.DV_FLAG.items():
+        assert int(defs["RYD_DV_" + k]) == v
+    for k, v in N.DV_LEAK.items():
+        assert int(defs["RYD_DV_LEAK_" + k.upper()]) == v
+    assert int(defs["RYD_DV_LEAK_OTHER"]) == N.DV_LEAK_OTHER
+    diag = {k: int(v) for k, v in defs.items() if k.startswith("RYD_DV_D_")}
+    assert sorted(diag.values()) == list(range(N.DV_NDIAG)) and int(defs["RYD_DV_NDIAG"]) == N.DV_NDIAG
+    # 8 int32 + 4 + 2 doubles + the species table + values + columns
+    assert ctypes.sizeof(N.DeriveDesc) == 32 + 48 + 8 * 24 * 4 + 8 * 38 + 4 * 38 + 0
 
 
 def test_library_loads_and_exports():
@@ -50,7 +63,7 @@ def test_library_loads_and_exports():
     lib = N.load()
     for sym in N.EXPORTED:
         assert hasattr(lib, sym), sym
-    assert lib.ryd_abi_version() == N.RYD_ABI_VERSION == 4
+    assert lib.ryd_abi_version() == N.RYD_ABI_VERSION == 5
     assert lib.ryd_param_count() == N.NPARAM
     assert lib.ryd_summary_width() == N.NSUMMARY
     assert lib.ryd_state_width(0, 3) == 25 and lib.ryd_state_width(1, 3) == 18
