@@ -9,7 +9,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Wall -Wno-unuse
 
 all: $(SO)
 
-$(SO): $(SRC) $(PKG)/csrc/ryd_traj.inc $(PKG)/csrc/ryd_traj_sym.inc $(PKG)/csrc/ryd_traj_eig.inc $(PKG)/csrc/ryd_traj_wg.inc $(PKG)/csrc/ryd_coh_prop.inc $(PKG)/csrc/ryd_dim4_prop.inc $(PKG)/csrc/ryd_shaped16.inc $(PKG)/csrc/ryd_generic.inc $(PKG)/csrc/ryd_sym16.inc $(PKG)/csrc/ryd_epilogue.inc $(PKG)/csrc/ryd_derive.inc include/ryd_engine.h
+$(SO): $(SRC) $(PKG)/csrc/ryd_traj.inc $(PKG)/csrc/ryd_traj_sym.inc $(PKG)/csrc/ryd_traj_eig.inc $(PKG)/csrc/ryd_traj_wg.inc $(PKG)/csrc/ryd_traj_rows.inc $(PKG)/csrc/ryd_coh_prop.inc $(PKG)/csrc/ryd_dim4_prop.inc $(PKG)/csrc/ryd_shaped16.inc $(PKG)/csrc/ryd_generic.inc $(PKG)/csrc/ryd_sym16.inc $(PKG)/csrc/ryd_epilogue.inc $(PKG)/csrc/ryd_derive.inc include/ryd_engine.h
 	$(HIPCC) $(HIPFLAGS) -o $@ $(SRC) -ldl
 
 resource-usage: $(SRC)

@@ -473,7 +473,7 @@ def run_c5(args, ws, rank, local, pg):
     eng = E.Engine(devices=[dev])
     db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=args.n_traj,
                                   ladder_levels=args.ladder if args.ladder >= 0 else TR.DEFAULT_LADDER,
-                                  seed=20260215, point_offset=off)
+                                  seed=20260215, point_offset=off, kernel=args.c5_kernel)
     for _ in range(args.warmup):
         db.launch()
     db.synchronize()
@@ -500,7 +500,8 @@ def run_c5(args, ws, rank, local, pg):
     napply = float(res.col("RESERVED").sum())
     exact = db.desc.ladder_levels == TR.N.T["EXACT"]
     wg = os.environ.get("RYD_T_WG", "0") == "1"
-    kernel = (("traj3w_kernel" if wg else "traj3e_kernel") if exact
+    rows = (args.c5_kernel == "rows" or (args.c5_kernel == "auto" and os.environ.get("RYD_T_ROWS", "0") != "0"))
+    kernel = (("traj3w_kernel" if wg else ("traj3r_kernel" if rows else "traj3e_kernel")) if exact
               else ("traj3s_kernel" if napply > 0 else "traj3_kernel"))
     if exact:                                       # traj3e_kernel: evaluations + basis changes
         ntr = args.n_traj
@@ -852,6 +853,8 @@ def main():
     ap.add_argument("--c5-shards", type=int, default=0,
                     help="C5: time rank --c5-rank's shard of an N-way split on this one GPU (0: off)")
     ap.add_argument("--c5-rank", type=int, default=0)
+    ap.add_argument("--c5-kernel", default="auto", choices=["auto", "rows", "lanes"],
+                    help="C5 exact-mode kernel: rows (traj3p + traj3r, 16-lane DPP rows), lanes (traj3e)")
     ap.add_argument("--c4-shards", type=int, default=0,
                     help="C4: time rank --c4-rank's shard of an N-way split on this one GPU (0: off)")
     ap.add_argument("--c4-rank", type=int, default=0)

@@ -193,6 +193,15 @@ extern "C" {
 #define RYD_TS_RESERVED    9     /* adapted-basis kernel: (I + X) applications; else 0 */
 #define RYD_T_NSUMMARY     10
 
+/* exact mode (ladder_levels = RYD_T_EXACT) kernel selection.  Both compute the same jump
+ * times (Newton on the eigen-decomposed H_eff) from the same Philox streams; they differ in
+ * the work mapping and so in the rounding of the sums (outputs agree to ~1e-15).  Every shard
+ * of a multi-GPU run must use the same one as its single-launch reference. */
+#define RYD_T_FLAG_ROWS  1u   /* one trajectory per 16-lane DPP row, pass 1 once per point
+                                 (traj3p_kernel + traj3r_kernel)                              */
+#define RYD_T_FLAG_LANES 2u   /* one trajectory per lane, points paired per wave, ranges
+                                 split over waves for small launches (traj3e_kernel); the
+                                 default                                                      */
 typedef struct ryd_traj_desc {
   int32_t abi_version;     /* = RYD_ABI_VERSION */
   int32_t protocol;        /* RYD_PROTO_* */
@@ -204,6 +213,8 @@ typedef struct ryd_traj_desc {
                               constant |Omega| and Delta (not a shaped LP envelope);
                               1 .. RYD_T_LADDER_MAX: the ladder walk, jump times
                               resolved to segment / 2^ladder_levels */
+  uint32_t flags;          /* RYD_T_FLAG_*: which exact-mode kernel (0: the library's default) */
+  uint32_t reserved;       /* 0 */
   uint64_t seed;
   double psi0[2 * RYD_T_DIM];  /* normalised initial ket, (re, im) interleaved */
 } ryd_traj_desc;

@@ -51,6 +51,8 @@ T = dict(DIM=27, RHO_WIDTH=1458, SE_WIDTH=729, EXACT=0, LADDER_MAX=40, REC_WIDTH
 TS = dict(MEAN_JUMPS=0, FRAC_JUMPED=1, MAX_JUMPS=2, TRACE=3, QUBIT_POP=4, ITER_USEFUL=5,
           ITER_EXEC=6, NLADDER=7, NSQUARE=8, RESERVED=9)
 T_NSUMMARY = 10
+# exact-mode kernel selection (ryd_traj_desc.flags)
+T_FLAG = {"auto": 0, "rows": 1, "lanes": 2}
 
 # ryd_last_timeline layout
 TL_HEAD, TL_SLOT = 4, 8
@@ -101,6 +103,7 @@ class TrajDesc(ctypes.Structure):
     _fields_ = [("abi_version", ctypes.c_int32), ("protocol", ctypes.c_int32),
                 ("shape", ctypes.c_int32), ("n_steps", ctypes.c_int32),
                 ("n_traj", ctypes.c_int32), ("ladder_levels", ctypes.c_int32),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
                 ("seed", ctypes.c_uint64), ("psi0", ctypes.c_double * 54)]
 
 

@@ -3395,34 +3395,35 @@ int ryd_derive(ryd_handle* h, const ryd_derive_desc* desc, const double* in, int
   const int dev = h->dev[0];
   hipStream_t s = h->stream[0];
   HIPCHK(hipSetDevice(dev));
-  hipMemPool_t pool = jp_pool(dev);
-  if (!pool) return fail(RYD_ERR_ALLOC, "derive: pool creation failed");
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t bIn = sizeof(double) * (size_t)n_cols * n, bP = sizeof(double) * RYD_NPARAM * (size_t)n,
                bW = sizeof(uint32_t) * (size_t)n, bD = diag ? sizeof(double) * RYD_DV_NDIAG * (size_t)n : 0;
   const size_t oP = al(bIn), oW = oP + al(bP), oD = oW + al(bW), tot = oD + al(bD) + 256;
-  // pageable host buffers: every copy is a blocking hipMemcpy issued after the stream work it
-  // depends on has completed (an async copy to or from pageable memory was observed to run
-  // ahead of the kernel on the same stream)
+  // a plain device allocation (host copies into the stream-ordered pool were observed to
+  // return stale data for large blocks), stream-ordered copies, the stream synchronised
+  // before the host reads anything
   char* buf = nullptr;
-  HIPCHK(hipMallocFromPoolAsync((void**)&buf, tot, pool, s));
-  hipError_t e = hipStreamSynchronize(s);
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMalloc((void**)&buf, tot));
+  hipError_t e = hipSuccess;
   for (int64_t c = 0; c < n_cols && e == hipSuccess; ++c)
-    e = hipMemcpy(buf + sizeof(double) * (size_t)c * n, in + c * ld_in, sizeof(double) * n, hipMemcpyHostToDevice);
+    e = hipMemcpyAsync(buf + sizeof(double) * (size_t)c * n, in + c * ld_in, sizeof(double) * n,
+                       hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
   int rc = RYD_OK;
   if (e == hipSuccess)
     rc = launch_derive(desc, (const double*)buf, n, n, (double*)(buf + oP), n, (uint32_t*)(buf + oW),
                        diag ? (double*)(buf + oD) : nullptr, n, s);
   if (e == hipSuccess && rc == RYD_OK) e = hipStreamSynchronize(s);
   for (int f = 0; f < RYD_NPARAM && e == hipSuccess && rc == RYD_OK; ++f)
-    e = hipMemcpy(params + f * ld_params, buf + oP + sizeof(double) * (size_t)f * n, sizeof(double) * n,
-                  hipMemcpyDeviceToHost);
-  if (e == hipSuccess && rc == RYD_OK) e = hipMemcpy(warn, buf + oW, bW, hipMemcpyDeviceToHost);
+    e = hipMemcpyAsync(params + f * ld_params, buf + oP + sizeof(double) * (size_t)f * n, sizeof(double) * n,
+                       hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess && rc == RYD_OK) e = hipMemcpyAsync(warn, buf + oW, bW, hipMemcpyDeviceToHost, s);
   for (int k = 0; diag && k < RYD_DV_NDIAG && e == hipSuccess && rc == RYD_OK; ++k)
-    e = hipMemcpy(diag + k * ld_diag, buf + oD + sizeof(double) * (size_t)k * n, sizeof(double) * n,
-                  hipMemcpyDeviceToHost);
-  const hipError_t ef = hipFreeAsync(buf, s);
+    e = hipMemcpyAsync(diag + k * ld_diag, buf + oD + sizeof(double) * (size_t)k * n, sizeof(double) * n,
+                       hipMemcpyDeviceToHost, s);
   const hipError_t es = hipStreamSynchronize(s);
+  const hipError_t ef = hipFree(buf);
   if (rc) return rc;
   if (e != hipSuccess) return fail(RYD_ERR_HIP, std::string("derive: ") + hipGetErrorString(e));
   if (ef != hipSuccess || es != hipSuccess) return fail(RYD_ERR_HIP, "derive: free/sync failed");

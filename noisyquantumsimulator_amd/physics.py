@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import warnings
 from dataclasses import dataclass, field
-from typing import Any, Dict, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -190,6 +190,59 @@ def _bc(x, n):
     return np.broadcast_to(np.asarray(x, dtype=float), (n,)).astype(float)
 
 
+# derive_batch's apparatus arguments that may be per-point arrays
+POINT_ARGS = ("species", "n_rydberg", "tweezer_power", "tweezer_waist", "tweezer_wavelength_nm",
+              "temperature", "B_field", "NA", "spacing_factor", "background_loss_rate_hz")
+
+
+def _per_point(key, v):
+    # bang-bang switching_times / phases given as one 1-D schedule are shared by all points
+    return np.ndim(v) > 0 and not (key in ("switching_times", "phases") and np.ndim(v) == 1)
+
+
+def batch_size(overrides=None, **kw) -> int:
+    """The point count derive_batch infers when ``n`` is None: the longest array argument."""
+    sizes = [np.size(v) for k, v in kw.items() if k in POINT_ARGS and v is not None and np.ndim(v) > 0]
+    sizes += [np.shape(v)[0] for k, v in (overrides or {}).items() if _per_point(k, v)]
+    return max(sizes) if sizes else 1
+
+
+def slice_inputs(kw: Dict[str, Any], n: int, lo: int, hi: int) -> Dict[str, Any]:
+    """derive_batch keyword arguments for points lo .. hi - 1 of an n-point call: every
+    per-point array (length n along its first axis) is sliced, everything else (scalars,
+    length-1 arrays that broadcast, shared schedules) passes through.  The derivation is
+    elementwise, so the slice's columns are the call's rows lo .. hi - 1."""
+    out = {}
+    for k, v in kw.items():
+        if k == "overrides" and v is not None:
+            out[k] = {ok: (ov[lo:hi] if _per_point(ok, ov) and np.shape(ov)[0] == n else ov)
+                      for ok, ov in v.items()}
+        elif k in POINT_ARGS and v is not None and np.ndim(v) > 0 and np.shape(v)[0] == n:
+            out[k] = v[lo:hi]
+        else:
+            out[k] = v
+    return out
+
+
+def concat_batches(parts: List["DerivedBatch"]) -> "DerivedBatch":
+    """One DerivedBatch from consecutive slices of a call (slice_inputs)."""
+    if len(parts) == 1:
+        return parts[0]
+    b0 = parts[0]
+    cat = lambda xs: None if xs[0] is None else np.concatenate(xs)
+    flags = []
+    for b in parts:
+        flags += [f for f in b.warnings if f not in flags]
+    return DerivedBatch(protocol=b0.protocol, pulse_shape=b0.pulse_shape, dim=b0.dim,
+                        include_noise=b0.include_noise, trap_laser_on=b0.trap_laser_on,
+                        n=sum(b.n for b in parts),
+                        cols={k: np.concatenate([b.cols[k] for b in parts]) for k in b0.cols},
+                        bangbang_times=cat([b.bangbang_times for b in parts]),
+                        bangbang_phases=cat([b.bangbang_phases for b in parts]),
+                        warnings=flags, noise_config=b0.noise_config,
+                        status_bits=cat([b.status_bits for b in parts]))
+
+
 def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
                  n_rydberg=70, qubit_0=(1, 0), qubit_1=(2, 0), hilbert_space_dim: int = 3,
                  tweezer_power=30e-3, tweezer_waist=1.0e-6, tweezer_wavelength_nm=None,
@@ -223,16 +276,11 @@ def derive_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
     if hilbert_space_dim not in (3, 4):
         raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
 
-    sizes = [np.size(a) for a in (n_rydberg, tweezer_power, tweezer_waist, temperature, B_field,
-                                  NA, spacing_factor) if np.ndim(a) > 0]
-    sizes += [np.shape(v)[0] for k, v in ov.items() if np.ndim(v) > 0
-              and not (k in ("switching_times", "phases") and np.ndim(v) == 1)]
-    if np.ndim(species) > 0:
-        sizes.append(np.size(species))
-    if tweezer_wavelength_nm is not None and np.ndim(tweezer_wavelength_nm) > 0:
-        sizes.append(np.size(tweezer_wavelength_nm))
     if n is None:
-        n = max(sizes) if sizes else 1
+        n = batch_size(species=species, n_rydberg=n_rydberg, tweezer_power=tweezer_power,
+                       tweezer_waist=tweezer_waist, tweezer_wavelength_nm=tweezer_wavelength_nm,
+                       temperature=temperature, B_field=B_field, NA=NA, spacing_factor=spacing_factor,
+                       overrides=ov)
     exc, noise = si.excitation, si.noise
     L1, L2 = exc.laser_1, exc.laser_2
     P1 = _bc(ov.get("laser_1_power", L1.power), n)

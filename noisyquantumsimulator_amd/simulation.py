@@ -421,6 +421,11 @@ def evolve_state_batch(H, psi0, T, c_ops=None, *, devices=None) -> np.ndarray:
 # none.  Ask for more with gauge_copies when the flag itself is the result being studied.
 BATCH_GAUGE_COPIES = 4
 
+# simulate_CZ_gate_batch's pipeline: up to PIPELINE_CHUNKS chunks of at least
+# PIPELINE_MIN_CHUNK points when the native epilogue runs (fewer points: one chunk)
+PIPELINE_CHUNKS = 4
+PIPELINE_MIN_CHUNK = 2048
+
 
 def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, species="Rb87",
                            n_rydberg=70, qubit_0=(1, 0), qubit_1=(2, 0), hilbert_space_dim: int = 3,
@@ -441,22 +446,26 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
         raise ValueError(f"Unsupported Hilbert space dimension: {hilbert_space_dim}. Use 3 or 4.")
     dim = hilbert_space_dim
     D = dim * dim
+    from concurrent.futures import ThreadPoolExecutor
     from . import engine as E
     t_start = time.perf_counter()
-    b = PH.derive_batch(simulation_inputs, n, species=species, n_rydberg=n_rydberg, qubit_0=qubit_0,
-                        qubit_1=qubit_1, hilbert_space_dim=hilbert_space_dim,
-                        tweezer_power=tweezer_power, tweezer_waist=tweezer_waist,
-                        tweezer_wavelength_nm=tweezer_wavelength_nm, temperature=temperature,
-                        B_field=B_field, NA=NA, spacing_factor=spacing_factor,
-                        include_noise=include_noise, background_loss_rate_hz=background_loss_rate_hz,
-                        trap_laser_on=trap_laser_on, overrides=overrides)
-    key = E.protocol_key(b)
-    shape = b.pulse_shape.lower() if key == "lp_shaped" else "square"
-    nn = b.n
-    g = b.channel_rates()
-    # mesolve with an empty c_op list evolves kets (RG/simulation.py:683-690)
-    ket_mask = (np.all([x == 0 for x in g], axis=0) & (b.mj_rate() == 0)) if include_noise \
-        else np.ones(nn, bool)
+    dkw = dict(species=species, n_rydberg=n_rydberg, qubit_0=qubit_0, qubit_1=qubit_1,
+               hilbert_space_dim=hilbert_space_dim, tweezer_power=tweezer_power,
+               tweezer_waist=tweezer_waist, tweezer_wavelength_nm=tweezer_wavelength_nm,
+               temperature=temperature, B_field=B_field, NA=NA, spacing_factor=spacing_factor,
+               include_noise=include_noise, background_loss_rate_hz=background_loss_rate_hz,
+               trap_laser_on=trap_laser_on, overrides=overrides)
+    nn = n if n is not None else PH.batch_size(**{k: v for k, v in dkw.items()
+                                                   if k in PH.POINT_ARGS or k == "overrides"})
+    host_eigh = phase_penalty == "reference" and eigh not in (None, "scipy")
+    native_epilogue = phase_penalty == "reference" and not host_eigh
+    # chunks: derivation and the GPU pass of chunk k + 1 run on this thread while the host
+    # LAPACK epilogue of chunk k runs on its pool (one ryd_mixed_phase call at a time, in
+    # chunk order; each rho's zheevr calls are the same as in one call, so the phases and
+    # flags are too).  The derivation is elementwise, so the chunks' columns are the
+    # whole call's (tests/test_pipeline_cpu.py).
+    k = min(PIPELINE_CHUNKS, nn // PIPELINE_MIN_CHUNK) if native_epilogue else 1
+    bounds = [(nn * c // k, nn * (c + 1) // k) for c in range(k)] if k > 1 else [(0, nn)]
     fids = np.zeros((nn, 4))
     pops = np.zeros((nn, 4))
     cp = np.full(nn, np.nan)
@@ -464,69 +473,94 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     fpro = np.full(nn, np.nan)
     fgate = np.full(nn, np.nan)
     phases = np.full((nn, 4), np.nan)
-    status = b.status_bits.copy() if b.status_bits is not None else np.zeros(nn, np.uint32)
+    status = np.zeros(nn, np.uint32)
+    ket_all = np.zeros(nn, bool)
     states = None
     if return_states:
         states = {"ket": np.zeros((nn, 4, D), complex), "rho": np.zeros((nn, 4, D, D), complex)}
     eng = _engine(devices)
     kms = 0.0
-    t_derived = time.perf_counter()
-    engine_s = 0.0
-    for evol, mask in (("ket", ket_mask), ("lindblad", ~ket_mask)):
-        idx = np.nonzero(mask)[0]
-        if idx.size == 0:
-            continue
+    derive_s = engine_s = 0.0
+    parts: List[PH.DerivedBatch] = []
+    pending = []                                    # (rows, future) of the epilogue calls
+    copies = gauge_copies if gauge_copies is not None else BATCH_GAUGE_COPIES
+
+    def epilogue(st, m):
         t0 = time.perf_counter()
-        prm = E.pack_params(b, idx)
-        r = eng.run(prm, key, evol, shape=shape, method=method if dim == 3 else "chebyshev", dim=dim)
-        coh = None
-        if process_fidelity and evol == "lindblad" and dim == 3:
-            coh, cst = eng.run_coherences(prm, key, shape=shape)
-            status[idx] |= cst
-        engine_s += time.perf_counter() - t0
-        if process_fidelity and (evol == "ket" or coh is not None):
-            from . import noise_models as NM
-            S = NM.ket_maps(r.kets(), dim) if evol == "ket" else NM.assemble_maps(r.state, coh)
-            fpro[idx], fgate[idx] = NM.gate_fidelity(S)
-        kms += r.kernel_ms
-        status[idx] |= r.status
-        P = r.populations()
-        pops[idx] = P
-        if evol == "ket":
-            cp[idx] = r.col("CTRL_PHASE")
-            pen[idx] = r.col("PENALTY")
-            if return_states:
-                states["ket"][idx] = r.kets()
-        else:
-            host_eigh = phase_penalty == "reference" and eigh not in (None, "scipy")
-            if phase_penalty == "reference" and not host_eigh:
-                ph, gflags = E.mixed_phase(r.state, idx.size, dim, gauge_check=gauge_check,
-                                           copies=gauge_copies if gauge_copies is not None else BATCH_GAUGE_COPIES)
-                cp[idx], pen[idx] = _cp_penalty(ph)
-                phases[idx] = ph
-                status[idx] |= gflags
-            need_rho = return_states or host_eigh
-            if need_rho:
-                for s0 in range(0, idx.size, 65536):
-                    sl = slice(s0, s0 + 65536)
-                    rho = E.expand_rho(r.state[:, 4 * s0:4 * (s0 + 65536)], min(65536, idx.size - s0), dim)
-                    if host_eigh:
-                        c_, p_ = mixed_phase_penalty(rho, eigh)
-                        cp[idx[sl]], pen[idx[sl]] = c_, p_
+        out = E.mixed_phase(st, m, dim, gauge_check=gauge_check, copies=copies)
+        return out, time.perf_counter() - t0
+
+    with ThreadPoolExecutor(max_workers=1) as ex:
+        for lo, hi in bounds:
+            t0 = time.perf_counter()
+            b = PH.derive_batch(simulation_inputs, hi - lo, **(PH.slice_inputs(dkw, nn, lo, hi) if k > 1 else dkw))
+            derive_s += time.perf_counter() - t0
+            parts.append(b)
+            key = E.protocol_key(b)
+            shape = b.pulse_shape.lower() if key == "lp_shaped" else "square"
+            g = b.channel_rates()
+            # mesolve with an empty c_op list evolves kets (RG/simulation.py:683-690)
+            ket_mask = (np.all([x == 0 for x in g], axis=0) & (b.mj_rate() == 0)) if include_noise \
+                else np.ones(b.n, bool)
+            ket_all[lo:hi] = ket_mask
+            if b.status_bits is not None:
+                status[lo:hi] |= b.status_bits
+            for evol, mask in (("ket", ket_mask), ("lindblad", ~ket_mask)):
+                loc = np.nonzero(mask)[0]
+                if loc.size == 0:
+                    continue
+                idx = lo + loc
+                t0 = time.perf_counter()
+                prm = E.pack_params(b, loc)
+                r = eng.run(prm, key, evol, shape=shape, method=method if dim == 3 else "chebyshev", dim=dim)
+                coh = None
+                if process_fidelity and evol == "lindblad" and dim == 3:
+                    coh, cst = eng.run_coherences(prm, key, shape=shape)
+                    status[idx] |= cst
+                engine_s += time.perf_counter() - t0
+                if process_fidelity and (evol == "ket" or coh is not None):
+                    from . import noise_models as NM
+                    S = NM.ket_maps(r.kets(), dim) if evol == "ket" else NM.assemble_maps(r.state, coh)
+                    fpro[idx], fgate[idx] = NM.gate_fidelity(S)
+                kms += r.kernel_ms
+                status[idx] |= r.status
+                pops[idx] = r.populations()
+                if evol == "ket":
+                    cp[idx] = r.col("CTRL_PHASE")
+                    pen[idx] = r.col("PENALTY")
                     if return_states:
-                        states["rho"][idx[sl]] = rho
+                        states["ket"][idx] = r.kets()
+                    continue
+                if native_epilogue:
+                    pending.append((idx, ex.submit(epilogue, r.state, idx.size)))
+                if return_states or host_eigh:
+                    for s0 in range(0, idx.size, 65536):
+                        sl = slice(s0, s0 + 65536)
+                        rho = E.expand_rho(r.state[:, 4 * s0:4 * (s0 + 65536)], min(65536, idx.size - s0), dim)
+                        if host_eigh:
+                            cp[idx[sl]], pen[idx[sl]] = mixed_phase_penalty(rho, eigh)
+                        if return_states:
+                            states["rho"][idx[sl]] = rho
+        epi_s = 0.0
+        for idx, fut in pending:
+            (ph, gflags), dt = fut.result()
+            epi_s += dt
+            cp[idx], pen[idx] = _cp_penalty(ph)
+            phases[idx] = ph
+            status[idx] |= gflags
+    b = PH.concat_batches(parts)
     fids[:] = pops
     fids[:, 3] = pops[:, 3] * pen
     avg = fids.mean(axis=1)
-    out_states = None
-    if return_states:
-        out_states = states
     t_end = time.perf_counter()
-    timings = {"derive_ms": (t_derived - t_start) * 1e3, "engine_ms": engine_s * 1e3,
-               "epilogue_ms": (t_end - t_derived - engine_s) * 1e3, "total_ms": (t_end - t_start) * 1e3}
+    # derive / engine / epilogue: each stage's own time (they overlap when chunked);
+    # total: the call's wall clock
+    timings = {"derive_ms": derive_s * 1e3, "engine_ms": engine_s * 1e3,
+               "epilogue_ms": (epi_s if native_epilogue else t_end - t_start - derive_s - engine_s) * 1e3,
+               "total_ms": (t_end - t_start) * 1e3, "chunks": len(bounds)}
     return BatchResult(batch=b, avg_fidelity=avg, fidelities=fids, populations=pops,
                        controlled_phase=cp, cz_phase_fidelity=pen, status=status,
-                       is_mixed=~ket_mask, states=out_states, kernel_ms=kms, timings=timings,
+                       is_mixed=~ket_all, states=states, kernel_ms=kms, timings=timings,
                        process_fidelity=fpro, avg_gate_fidelity=fgate, phases=phases)
 
 

@@ -91,8 +91,14 @@ def _psi_array(psi0: np.ndarray) -> np.ndarray:
 
 def make_traj_desc(protocol: str, psi0: np.ndarray, n_traj: int = 256, seed: int = 0,
                    ladder_levels: Optional[int] = DEFAULT_LADDER, n_steps: int = 0,
-                   shape: str = "square") -> N.TrajDesc:
+                   shape: str = "square", kernel: str = "auto") -> N.TrajDesc:
+    """``kernel`` picks the exact-mode kernel (include/ryd_engine.h RYD_T_FLAG_*): "rows"
+    (one trajectory per 16-lane DPP row, pass 1 once per point), "lanes" (one trajectory per
+    lane, traj3e), or "auto" (the library's default, lanes; env RYD_T_ROWS=1 -> rows)."""
+    if kernel not in N.T_FLAG:
+        raise ValueError(f"kernel must be one of {sorted(N.T_FLAG)}")
     d = N.TrajDesc()
+    d.flags = N.T_FLAG[kernel]
     d.abi_version = N.RYD_ABI_VERSION
     d.protocol = N.PROTO[protocol]
     d.shape = N.SHAPE[shape]
@@ -155,7 +161,7 @@ class TrajectoryResult:
 def run_trajectories(engine: Engine, params: np.ndarray, protocol: str, psi0: Optional[np.ndarray] = None,
                      n_traj: int = 256, seed: int = 0, ladder_levels: Optional[int] = DEFAULT_LADDER,
                      n_steps: Optional[int] = None, shape: str = "square",
-                     records: bool = False) -> TrajectoryResult:
+                     records: bool = False, kernel: str = "auto") -> TrajectoryResult:
     """Host-buffer form: every point of ``params`` (``pack_params`` columns; atom-A
     rates are used for all three atoms) through ``n_traj`` trajectories."""
     params = np.ascontiguousarray(params, dtype=np.float64)
@@ -165,7 +171,7 @@ def run_trajectories(engine: Engine, params: np.ndarray, protocol: str, psi0: Op
     if n_steps is None:
         n_steps = default_n_steps(protocol, params)
     desc = make_traj_desc(protocol, plus_state() if psi0 is None else psi0, n_traj, seed, ladder_levels,
-                          n_steps, shape)
+                          n_steps, shape, kernel)
     rho = np.zeros((n, N.T["RHO_WIDTH"]))
     se = np.zeros((n, N.T["SE_WIDTH"]))
     summ = np.zeros((N.T_NSUMMARY, n))
@@ -188,7 +194,7 @@ class TrajectoryDeviceBatch:
     def __init__(self, engine: Engine, params: np.ndarray, protocol: str, psi0: Optional[np.ndarray] = None,
                  n_traj: int = 256, seed: int = 0, ladder_levels: Optional[int] = DEFAULT_LADDER,
                  n_steps: Optional[int] = None, shape: str = "square", slot: int = 0,
-                 point_offset: int = 0, records: bool = False):
+                 point_offset: int = 0, records: bool = False, kernel: str = "auto"):
         self.eng, self.slot, self.point_offset = engine, slot, point_offset
         lib = engine.lib
         params = np.ascontiguousarray(params, dtype=np.float64)
@@ -197,7 +203,7 @@ class TrajectoryDeviceBatch:
             n_steps = default_n_steps(protocol, params)
         self.n_traj = n_traj
         self.desc = make_traj_desc(protocol, plus_state() if psi0 is None else psi0, n_traj, seed,
-                                   ladder_levels, n_steps, shape)
+                                   ladder_levels, n_steps, shape, kernel)
         self._bufs = []
 
         def alloc(nbytes):

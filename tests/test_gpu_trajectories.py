@@ -47,6 +47,10 @@ def _two_atom(si, n=2):
 
 
 LADDERS = [16, N.T["EXACT"]]          # the ladder walk and the exact-jump-time kernel
+# (ladder_levels, exact-mode kernel): the ladder, traj3e (one trajectory per lane, the
+# default) and traj3r (one trajectory per 16-lane DPP row, include/ryd_engine.h RYD_T_FLAG_ROWS)
+MODES = [(16, "auto"), (N.T["EXACT"], "lanes"), (N.T["EXACT"], "rows")]
+EXACT_KERNELS = ["lanes", "rows"]
 
 
 @pytest.mark.parametrize("ladder", LADDERS)
@@ -163,15 +167,16 @@ def test_trajectories_match_exact_time_oracle(eng):
     assert checked > 5
 
 
+@pytest.mark.parametrize("kernel", EXACT_KERNELS)
 @pytest.mark.parametrize("idx,scale", [(1200, 40.0), (77, 60.0), (4095, 40.0)])
-def test_exact_jump_times_match_oracle(eng, idx, scale):
+def test_exact_jump_times_match_oracle(eng, idx, scale, kernel):
     """ladder_levels = RYD_T_EXACT: every jump time is the root the oracle's brentq finds
     (Newton on the eigen-decomposed H_eff), not the end of a ladder quantum -- so later
     jumps agree as tightly as the first, and so do the final kets."""
     p = _c5([idx], scale=scale)
     psi0 = TR.plus_state()
     r = TR.run_trajectories(eng, p, "lp_square", psi0, n_traj=256, seed=77, ladder_levels=N.T["EXACT"],
-                            records=True)
+                            records=True, kernel=kernel)
     assert r.status[0] == 0
     nj, tj, cj, kets = r.n_jumps()[0], r.jump_times()[0], r.jump_channels()[0], r.kets()[0]
     dt = p[N.P["TAU"], 0]
@@ -187,10 +192,10 @@ def test_exact_jump_times_match_oracle(eng, idx, scale):
     assert checked > 5
 
 
-@pytest.mark.parametrize("ladder", LADDERS)
-def test_launch_shape_and_partition_independence(eng, ladder):
+@pytest.mark.parametrize("ladder,kernel", MODES)
+def test_launch_shape_and_partition_independence(eng, ladder, kernel):
     p = _c5(list(range(0, 4096, 512)), scale=20.0)
-    kw = dict(ladder_levels=ladder)
+    kw = dict(ladder_levels=ladder, kernel=kernel)
     a = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=5, records=True, **kw)
     b = TR.run_trajectories(eng, p, "lp_square", n_traj=512, seed=5, records=True, **kw)
     np.testing.assert_array_equal(a.records, b.records[:, :256])     # a trajectory = its stream
@@ -279,11 +284,11 @@ def test_bad_inputs(eng, ladder):
             ladder_levels=N.T["EXACT"])
 
 
-@pytest.mark.parametrize("ladder", LADDERS)
-def test_c5_full_grid_properties(eng, ladder):
+@pytest.mark.parametrize("ladder,kernel", MODES)
+def test_c5_full_grid_properties(eng, ladder, kernel):
     warnings.simplefilter("ignore")
     p = E.pack_params(SW.blockade_grid_3atom())
-    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=20260215, ladder_levels=ladder)
+    r = TR.run_trajectories(eng, p, "lp_square", n_traj=256, seed=20260215, ladder_levels=ladder, kernel=kernel)
     assert r.n == 4096 and np.all(r.status == 0)
     np.testing.assert_allclose(r.col("TRACE"), 1.0, atol=1e-12)
     np.testing.assert_allclose(r.rho, np.conj(np.transpose(r.rho, (0, 2, 1))), atol=0)
@@ -300,7 +305,7 @@ def test_c5_full_grid_properties(eng, ladder):
     for rank in (0, 5):
         b, off = SW.c5_rank_shard(rank, 8)
         db = TR.TrajectoryDeviceBatch(eng, E.pack_params(b), "lp_square", n_traj=256, seed=20260215,
-                                      point_offset=off, ladder_levels=ladder)
+                                      point_offset=off, ladder_levels=ladder, kernel=kernel)
         db.launch()
         db.synchronize()
         o = db.fetch()
@@ -310,3 +315,20 @@ def test_c5_full_grid_properties(eng, ladder):
         # (ITER_EXEC counts the issued row-evaluations: scheduling-dependent in the exact kernel)
         det = [N.TS[k] for k in ("MEAN_JUMPS", "FRAC_JUMPED", "MAX_JUMPS", "TRACE", "QUBIT_POP", "ITER_USEFUL")]
         np.testing.assert_array_equal(o.summary[det], r.summary[det][:, off:off + o.n])
+
+
+def test_exact_kernels_agree(eng):
+    """traj3r and traj3e walk the same Philox streams to the same jump times; they differ
+    only in the order of the floating-point sums (one row per trajectory vs one lane), so the
+    outputs agree to rounding and the jump records exactly in count and channel."""
+    warnings.simplefilter("ignore")
+    p = E.pack_params(SW.blockade_grid_3atom())[:, ::8].copy()
+    kw = dict(n_traj=256, seed=20260215, ladder_levels=N.T["EXACT"], records=True)
+    a = TR.run_trajectories(eng, p, "lp_square", kernel="lanes", **kw)
+    b = TR.run_trajectories(eng, p, "lp_square", kernel="rows", **kw)
+    assert np.all(a.status == 0) and np.all(b.status == 0)
+    np.testing.assert_allclose(b.rho, a.rho, atol=1e-12, rtol=0)
+    np.testing.assert_allclose(b.se, a.se, atol=1e-12, rtol=0)
+    np.testing.assert_array_equal(b.n_jumps(), a.n_jumps())
+    np.testing.assert_array_equal(b.jump_channels(), a.jump_channels())
+    np.testing.assert_allclose(b.jump_times(), a.jump_times(), atol=1e-12 * float(p[N.P["TAU"]].max()), rtol=0)

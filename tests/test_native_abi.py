@@ -41,7 +41,8 @@ def test_header_constants_match_binding():
         assert int(defs["RYD_TS_" + k]) == v
     assert int(defs["RYD_T_NSUMMARY"]) == N.T_NSUMMARY
     assert int(defs["RYD_ABI_VERSION"]) == N.RYD_ABI_VERSION
-    assert ctypes.sizeof(N.TrajDesc) == 464
+    assert ctypes.sizeof(N.TrajDesc) == 472
+    assert int(defs["RYD_T_FLAG_ROWS"]) == N.T_FLAG["rows"] and int(defs["RYD_T_FLAG_LANES"]) == N.T_FLAG["lanes"]
     for k, v in N.DV.items():
         assert int(defs["RYD_DV_" + k]) == v
     assert int(defs["RYD_DV_NFIELD"]) == N.DV_NFIELD and int(defs["RYD_DV_NSPC"]) == N.DV_NSPC

@@ -129,7 +129,7 @@ def test_c5_grid_and_shards():
 
 
 def test_traj_desc_layout_and_states():
-    assert ctypes.sizeof(N.TrajDesc) == 464
+    assert ctypes.sizeof(N.TrajDesc) == 472                # ABI 5: flags + reserved before the seed
     d = TR.make_traj_desc("lp_square", TR.plus_state(), 512, seed=3)
     v = np.array(d.psi0[:])
     assert abs((v ** 2).sum() - 1) < 1e-15 and d.n_traj == 512 and d.ladder_levels == N.T["EXACT"]
