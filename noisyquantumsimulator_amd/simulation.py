@@ -465,7 +465,11 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
     # flags are too).  The derivation is elementwise, so the chunks' columns are the
     # whole call's (tests/test_pipeline_cpu.py).
     k = min(PIPELINE_CHUNKS, nn // PIPELINE_MIN_CHUNK) if native_epilogue else 1
-    bounds = [(nn * c // k, nn * (c + 1) // k) for c in range(k)] if k > 1 else [(0, nn)]
+    bounds = [(0, nn)]
+    if k > 1:
+        # the first chunk is half the others: the epilogue pool starts sooner
+        f = nn // (2 * k - 1)
+        bounds = [(0, f)] + [(f + (nn - f) * c // (k - 1), f + (nn - f) * (c + 1) // (k - 1)) for c in range(k - 1)]
     fids = np.zeros((nn, 4))
     pops = np.zeros((nn, 4))
     cp = np.full(nn, np.nan)
