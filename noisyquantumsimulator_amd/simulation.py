@@ -545,6 +545,7 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
                             cp[idx[sl]], pen[idx[sl]] = mixed_phase_penalty(rho, eigh)
                         if return_states:
                             states["rho"][idx[sl]] = rho
+        b = PH.concat_batches(parts)                # (while the last epilogue runs)
         epi_s = 0.0
         for idx, fut in pending:
             (ph, gflags), dt = fut.result()
@@ -552,7 +553,6 @@ def simulate_CZ_gate_batch(simulation_inputs, n: Optional[int] = None, *, specie
             cp[idx], pen[idx] = _cp_penalty(ph)
             phases[idx] = ph
             status[idx] |= gflags
-    b = PH.concat_batches(parts)
     fids[:] = pops
     fids[:, 3] = pops[:, 3] * pen
     avg = fids.mean(axis=1)
