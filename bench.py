@@ -469,17 +469,21 @@ def run_c5(args, ws, rank, local, pg):
     from noisyquantumsimulator_amd import engine as E
     from noisyquantumsimulator_amd import sweeps as SW
     from noisyquantumsimulator_amd import trajectories as TR
-    if args.c5_shards:           # one GPU, one rank's shard of an N-way split (the scaling proxy)
-        batch, off = SW.c5_rank_shard(args.c5_rank, args.c5_shards, order=args.c5_order)
+    # --c5-shards: one GPU, one rank's shard of an N-way split (the scaling proxy);
+    # --c5-order strided: rank r takes points r, r + N, ... of the Omega-major grid
+    r_, ws_ = (args.c5_rank, args.c5_shards) if args.c5_shards else (rank, ws)
+    stride = 1
+    if args.c5_order == "strided":
+        batch, off, stride = SW.c5_strided_shard(r_, ws_)
     else:
-        batch, off = SW.c5_rank_shard(rank, ws, order=args.c5_order)
+        batch, off = SW.c5_rank_shard(r_, ws_, order=args.c5_order)
     params = E.pack_params(batch)
     n = batch.n
     dev = _rank_device(local)
     eng = E.Engine(devices=[dev])
     db = TR.TrajectoryDeviceBatch(eng, params, "lp_square", TR.plus_state(), n_traj=args.n_traj,
                                   ladder_levels=args.ladder if args.ladder >= 0 else TR.DEFAULT_LADDER,
-                                  seed=20260215, point_offset=off, kernel=args.c5_kernel)
+                                  seed=20260215, point_offset=off, kernel=args.c5_kernel, point_stride=stride)
     for _ in range(args.warmup):
         db.launch()
     db.synchronize()
@@ -864,8 +868,9 @@ def main():
     ap.add_argument("--c4-shards", type=int, default=0,
                     help="C4: time rank --c4-rank's shard of an N-way split on this one GPU (0: off)")
     ap.add_argument("--c4-rank", type=int, default=0)
-    ap.add_argument("--c5-order", default="omega", choices=["omega", "blocked", "balanced"],
-                    help="C5 grid point order (sweeps.blockade_grid_3atom)")
+    ap.add_argument("--c5-order", default="omega", choices=["omega", "blocked", "balanced", "strided"],
+                    help="C5 grid point order (sweeps.blockade_grid_3atom); strided: the Omega-major "
+                         "grid split over the ranks by point index mod N (sweeps.c5_strided_shard)")
     ap.add_argument("--ladder", type=int, default=-1,
                     help="C5 ladder levels (0: exact jump times; -1: trajectories.DEFAULT_LADDER)")
     ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)   # launcher test: no GPU

@@ -214,7 +214,10 @@ typedef struct ryd_traj_desc {
                               1 .. RYD_T_LADDER_MAX: the ladder walk, jump times
                               resolved to segment / 2^ladder_levels */
   uint32_t flags;          /* RYD_T_FLAG_*: which exact-mode kernel (0: the library's default) */
-  uint32_t reserved;       /* 0 */
+  uint32_t point_stride;   /* global index of point i = point_offset + point_stride * i (the
+                              trajectories' random-stream key); 0 and 1: contiguous.  A strided
+                              shard (rank r of N: offset r, stride N) reproduces rows r, r + N,
+                              ... of the whole launch */
   uint64_t seed;
   double psi0[2 * RYD_T_DIM];  /* normalised initial ket, (re, im) interleaved */
 } ryd_traj_desc;

@@ -103,7 +103,7 @@ class TrajDesc(ctypes.Structure):
     _fields_ = [("abi_version", ctypes.c_int32), ("protocol", ctypes.c_int32),
                 ("shape", ctypes.c_int32), ("n_steps", ctypes.c_int32),
                 ("n_traj", ctypes.c_int32), ("ladder_levels", ctypes.c_int32),
-                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("point_stride", ctypes.c_uint32),
                 ("seed", ctypes.c_uint64), ("psi0", ctypes.c_double * 54)]
 
 

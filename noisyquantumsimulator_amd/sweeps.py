@@ -260,6 +260,18 @@ def c5_rank_shard(rank: int, world_size: int, include_noise: bool = True, order:
     return blockade_grid_3atom(include_noise=include_noise, point_slice=sl, order=order), sl.start
 
 
+def c5_strided_shard(rank: int, world_size: int, include_noise: bool = True):
+    """Strided shard of the Omega-major C5 grid: points rank, rank + N, rank + 2N, ... --
+    (batch, offset, stride) for TrajectoryDeviceBatch(point_offset=offset, point_stride=
+    stride).  Every rank then spans the whole Omega axis (the ranks' loads even out) while
+    each shard keeps the Omega-major order its launch packs best, and the single launch of
+    the whole grid stays the Omega-major one."""
+    if not 0 <= rank < world_size:
+        raise ValueError("rank out of range")
+    return (blockade_grid_3atom(include_noise=include_noise, point_slice=slice(rank, C5_POINTS, world_size)),
+            rank, world_size)
+
+
 def range_shard(n: int, rank: int, world_size: int) -> slice:
     """Contiguous range partition: point i -> rank floor(world_size * i / n)."""
     if not 0 <= rank < world_size:

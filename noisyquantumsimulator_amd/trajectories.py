@@ -189,12 +189,16 @@ def run_trajectories(engine: Engine, params: np.ndarray, protocol: str, psi0: Op
 
 class TrajectoryDeviceBatch:
     """Inputs resident in HBM on one device slot, for timed re-runs (bench.py) and
-    range shards launched with their global ``point_offset``."""
+    shards launched with their global point indices: point i of the batch is global point
+    ``point_offset + point_stride * i`` (a range shard: stride 1; rank r of a strided split
+    over N ranks: offset r, stride N), which keys its trajectories' random streams."""
 
     def __init__(self, engine: Engine, params: np.ndarray, protocol: str, psi0: Optional[np.ndarray] = None,
                  n_traj: int = 256, seed: int = 0, ladder_levels: Optional[int] = DEFAULT_LADDER,
                  n_steps: Optional[int] = None, shape: str = "square", slot: int = 0,
-                 point_offset: int = 0, records: bool = False, kernel: str = "auto"):
+                 point_offset: int = 0, records: bool = False, kernel: str = "auto", point_stride: int = 1):
+        if point_stride < 1 or point_offset < 0:
+            raise ValueError("point_stride must be >= 1 and point_offset >= 0")
         self.eng, self.slot, self.point_offset = engine, slot, point_offset
         lib = engine.lib
         params = np.ascontiguousarray(params, dtype=np.float64)
@@ -204,6 +208,7 @@ class TrajectoryDeviceBatch:
         self.n_traj = n_traj
         self.desc = make_traj_desc(protocol, plus_state() if psi0 is None else psi0, n_traj, seed,
                                    ladder_levels, n_steps, shape, kernel)
+        self.desc.point_stride = point_stride
         self._bufs = []
 
         def alloc(nbytes):

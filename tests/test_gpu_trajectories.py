@@ -315,6 +315,19 @@ def test_c5_full_grid_properties(eng, ladder, kernel):
         # (ITER_EXEC counts the issued row-evaluations: scheduling-dependent in the exact kernel)
         det = [N.TS[k] for k in ("MEAN_JUMPS", "FRAC_JUMPED", "MAX_JUMPS", "TRACE", "QUBIT_POP", "ITER_USEFUL")]
         np.testing.assert_array_equal(o.summary[det], r.summary[det][:, off:off + o.n])
+    # strided shards (sweeps.c5_strided_shard: points r, r + 8, ...; point_stride keys the
+    # random streams by global index) reproduce rows r::8 of the same launch
+    for rank in (0, 5):
+        b, off, stride = SW.c5_strided_shard(rank, 8)
+        db = TR.TrajectoryDeviceBatch(eng, E.pack_params(b), "lp_square", n_traj=256, seed=20260215,
+                                      point_offset=off, point_stride=stride, ladder_levels=ladder, kernel=kernel)
+        db.launch()
+        db.synchronize()
+        o = db.fetch()
+        db.free()
+        np.testing.assert_array_equal(o.rho, r.rho[rank::8])
+        np.testing.assert_array_equal(o.se, r.se[rank::8])
+        np.testing.assert_array_equal(o.summary[det], r.summary[det][:, rank::8])
 
 
 def test_exact_kernels_agree(eng):

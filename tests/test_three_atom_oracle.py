@@ -129,7 +129,7 @@ def test_c5_grid_and_shards():
 
 
 def test_traj_desc_layout_and_states():
-    assert ctypes.sizeof(N.TrajDesc) == 472                # ABI 5: flags + reserved before the seed
+    assert ctypes.sizeof(N.TrajDesc) == 472                # ABI 5: flags + point_stride before the seed
     d = TR.make_traj_desc("lp_square", TR.plus_state(), 512, seed=3)
     v = np.array(d.psi0[:])
     assert abs((v ** 2).sum() - 1) < 1e-15 and d.n_traj == 512 and d.ladder_levels == N.T["EXACT"]
@@ -141,3 +141,18 @@ def test_traj_desc_layout_and_states():
     flat = np.arange(1458, dtype=float)[None]
     rho = TR.unpack_rho(flat)
     assert rho[0, 1, 0] == 2 + 3j and rho[0, 0, 1] == 54 + 55j    # vec index a + 27 b
+
+
+def test_strided_shards_partition_the_grid():
+    """sweeps.c5_strided_shard: rank r of N holds points r, r + N, ... (offset r, stride N);
+    together the ranks hold every point of the Omega-major grid once, with its columns."""
+    full = E.pack_params(SW.blockade_grid_3atom())
+    seen = np.zeros(SW.C5_POINTS, int)
+    for r in range(8):
+        b, off, stride = SW.c5_strided_shard(r, 8)
+        assert (off, stride) == (r, 8) and b.n == SW.C5_POINTS // 8
+        np.testing.assert_array_equal(E.pack_params(b), full[:, r::8])
+        seen[r::8] += 1
+    assert np.all(seen == 1)
+    d = TR.make_traj_desc("lp_square", TR.plus_state(), 256)
+    assert d.point_stride == 0                     # contiguous unless a shard sets it
